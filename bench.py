@@ -1,0 +1,175 @@
+#!/usr/bin/env python3
+"""bench.py -- agent-steps/s of the MI355X madrona-bots world step.
+
+One "step" = Manager::step() (Step + Sensor graphs, sim.cpp:1061-1188) +
+shift_observations() (sim.cpp:1190-1220) + writing the next one-hot actions
+for every live agent (the learner's write, learn/env.py:94-98), on synthetic
+identity-keyed actions.  Worlds are sharded across ranks with
+no collective on the step (weak scaling: `--worlds` per GPU, default 65536 =
+BASELINE config 3).  Rank 0 prints one JSON line.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--worlds WPG]
+    torchrun --nproc-per-node N bench.py --gpus N ...
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "madrona-bots_amd"))
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0       # MI355X HBM3E spec (MI355X_MICROARCH.md)
+SEED = 69                   # learn/env.py:15
+ACTION_SEED = 1234
+AGENTS_PER_WORLD = 32       # learn/env.py:15
+
+
+def algorithmic_bytes(kernel, n_agents, n_worlds):
+    """B_step = 552 N + 1952 W, split per kernel."""
+    if kernel == "shift":
+        return 264.0 * n_agents
+    return 288.0 * n_agents + 1952.0 * n_worlds
+
+
+def cpu_baseline(worlds_sample, target_s):
+    """The C oracle (oracle/, test infrastructure) on host cores: a bounded
+    sample of the same workload (same seed/actions), world-parallel threads."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle
+    threads = max(1, min(16, os.cpu_count() or 1))
+    sim = pyoracle.OracleSim(worlds_sample, SEED, AGENTS_PER_WORLD, cap=128, num_threads=threads)
+    agent_steps, steps = 0, 0
+    t0 = time.perf_counter()
+    while True:
+        sim.write_synthetic_actions(ACTION_SEED, steps)
+        sim.step()
+        sim.shift_observations()
+        agent_steps += sim.num_agents()
+        steps += 1
+        dt = time.perf_counter() - t0
+        if dt >= target_s or steps >= 2000:
+            break
+    return {"value": agent_steps / dt, "unit": "agent-steps/s", "cores": threads,
+            "kind": "port",
+            "sample": f"{worlds_sample} worlds x {AGENTS_PER_WORLD} agents, {steps} steps "
+                      f"(step+shift+actions), oracle/mbots_oracle.c on {threads} threads, "
+                      f"{dt:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--worlds", type=int, default=65536, help="worlds per GPU")
+    ap.add_argument("--cpu-worlds", type=int, default=1024)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-kernel-timing", action="store_true")
+    args = ap.parse_args()
+
+    world_size = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    distributed = world_size > 1
+    if distributed:
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", local_rank)
+
+    import madrona_bots as mb
+    W = args.worlds
+    mgr = mb.SimManager(local_rank, W, SEED, AGENTS_PER_WORLD, world_offset=rank * W)
+
+    def one_step(t):
+        mgr.step()
+        mgr.shift_observations()
+        mgr.write_synthetic_actions(ACTION_SEED, t + 1)
+
+    mgr.write_synthetic_actions(ACTION_SEED, 0)
+    for t in range(args.warmup):
+        one_step(t)
+    torch.cuda.synchronize()
+    steps_before = mgr.agent_steps()
+    if not args.no_kernel_timing:
+        mgr.enable_kernel_timing(True)
+
+    if distributed:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for t in range(args.warmup, args.warmup + args.steps):
+        one_step(t)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    if distributed:
+        dist.barrier()
+    elapsed = t1 - t0
+
+    agent_steps = mgr.agent_steps() - steps_before
+    ktimes = mgr.kernel_times() if not args.no_kernel_timing else {}
+    stats = torch.tensor([elapsed, float(agent_steps)], dtype=torch.float64, device=dev)
+    if distributed:
+        tmax = stats[0:1].clone()
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+        tot = stats[1:2].clone()
+        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+        elapsed, total_agent_steps = float(tmax.item()), float(tot.item())
+    else:
+        total_agent_steps = float(agent_steps)
+
+    if rank == 0:
+        mean_agents = agent_steps / args.steps          # this rank's mean population
+        value = total_agent_steps / elapsed
+        out = {
+            "metric": "agent-steps/sec at 4096 & 65536 worlds; 1/2/4/8 MI355X scaling",
+            "value": value,
+            "unit": "agent-steps/s",
+            "n_gpus": world_size,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (identity-keyed one-hot action stream, seed 69)",
+            "config": {"workload": f"{W} worlds/GPU x {AGENTS_PER_WORLD} initial agents "
+                                   f"(BASELINE config {'3' if W == 65536 else 'custom'}), "
+                                   "step+shift+action write",
+                       "worlds_per_gpu": W, "total_worlds": W * world_size,
+                       "mean_agents_per_world": mean_agents / W,
+                       "world_steps_per_s": W * world_size * args.steps / elapsed,
+                       "parallelism": f"world-shard x{world_size}, no collective"},
+        }
+        if ktimes:
+            per = {k: (ms / n if n else 0.0) for k, (ms, n) in ktimes.items()}
+            out["kernel_ms"] = {k: round(v, 5) for k, v in per.items()}
+            step_ms = sum(per[k] for k in ("world_step", "scan", "export", "sensor"))
+            shift_ms = per["shift"]
+            cand = {"step": step_ms, "shift": shift_ms}
+            dom = max(cand, key=cand.get)
+            nb = algorithmic_bytes(dom, mean_agents, W)
+            achieved = nb / (cand[dom] * 1e-3) / 1e9
+            out["roofline"] = {"bound": "hbm", "kernel": dom, "achieved": achieved,
+                               "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                               "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                               "algorithmic_bytes_per_launch": nb,
+                               "avg_launch_ms": cand[dom]}
+        if not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(args.cpu_worlds, args.cpu_seconds)
+        print(json.dumps(out), flush=True)
+
+    if distributed:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

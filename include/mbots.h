@@ -1,0 +1,147 @@
+/*
+ * mbots.h -- C ABI of the MI355X-native madrona-bots simulator (libmbots.so).
+ *
+ * This is the drop-in boundary for the reference's host surface:
+ *   class Manager            src/entry/mgr.hpp:10-68
+ *   Manager::Impl::make      src/entry/mgr.cpp:166-240
+ *   nanobind SimManager      src/entry/entry.cpp:16-45
+ * Plain pointers, sizes and status codes only (no torch / HIP C++ types).
+ * Every function returns MBOTS_OK (0) or a negative MBOTS_E* code; the text of
+ * the last error on the calling thread is available from mbots_last_error().
+ * Streams are passed as `void *` holding a hipStream_t (NULL = default stream).
+ *
+ * Ownership (mgr.cpp:138-144): the handle owns every device buffer; tensors
+ * returned by mbots_export are non-owning views that stay valid until the next
+ * mbots_step (the export tables are double-buffered and swap on every step;
+ * the reference's views are likewise shape-stale after step()).
+ */
+#ifndef MBOTS_H
+#define MBOTS_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MBOTS_OK             0
+#define MBOTS_E_INVALID    (-1)   /* bad argument / config             */
+#define MBOTS_E_HIP        (-2)   /* HIP runtime error                  */
+#define MBOTS_E_NOMEM      (-3)   /* device / host allocation failed    */
+#define MBOTS_E_RANGE      (-4)   /* index out of range                 */
+
+/* Manager::Config flags (build extensions; default 0 = reference-faithful) */
+#define MBOTS_FLAG_REWARD_FIXED     0x1u  /* rewards[speciesID-1] (fixes sim.cpp:943) */
+#define MBOTS_FLAG_FIX_DEPTH_ALIAS  0x2u  /* depth_tensor exports real depth (sim.cpp:102-112) */
+
+/* Manager::Config (src/entry/mgr.hpp:12-23) plus sharding / capacity knobs. */
+typedef struct mbots_config {
+    int32_t  gpu_id;                    /* gpuID                              */
+    uint32_t num_worlds;                /* numWorlds held by this instance    */
+    uint32_t rand_seed;                 /* randSeed                           */
+    uint32_t init_num_agents_per_world; /* initNumAgentsPerWorld              */
+    uint32_t sensor_size;               /* sensorSize; must be 32             */
+    uint32_t world_offset;              /* global index of world 0 (shards)   */
+    uint32_t agent_capacity;            /* per-world slot cap (0 -> 128)      */
+    uint32_t flags;                     /* MBOTS_FLAG_*                       */
+} mbots_config;
+
+/* Export slots; numbering mirrors enum class ExportID (src/sim/sim.hpp:18-55). */
+enum mbots_export_id {
+    MBOTS_EXPORT_RESET = 0,
+    MBOTS_EXPORT_ACTION = 1,
+    MBOTS_EXPORT_PREV_ACTION = 2,
+    MBOTS_EXPORT_HIDDEN_STATE = 3,
+    MBOTS_EXPORT_PREV_HIDDEN_STATE = 4,
+    MBOTS_EXPORT_REWARD = 5,
+    MBOTS_EXPORT_PREV_REWARD = 6,
+    MBOTS_EXPORT_DONE = 7,
+    MBOTS_EXPORT_POSITION = 8,
+    MBOTS_EXPORT_PREV_POSITION = 9,
+    MBOTS_EXPORT_HEALTH = 10,
+    MBOTS_EXPORT_PREV_HEALTH = 11,
+    MBOTS_EXPORT_SURROUNDING = 12,
+    MBOTS_EXPORT_PREV_SURROUNDING = 13,
+    MBOTS_EXPORT_SENSOR_SEMANTIC = 14,
+    MBOTS_EXPORT_SENSOR_DEPTH = 15,
+    MBOTS_EXPORT_PREV_SENSOR_SEMANTIC = 16,
+    MBOTS_EXPORT_PREV_SENSOR_DEPTH = 17,
+    MBOTS_EXPORT_STATS = 18,
+    MBOTS_EXPORT_PREV_STATS = 19,
+    MBOTS_EXPORT_SENSOR_INDEX = 20,
+    MBOTS_EXPORT_SPECIES_COUNT = 21,
+    MBOTS_EXPORT_NUM_REFERENCE = 22,
+    /* build extensions (not exported by the reference) */
+    MBOTS_EXPORT_SPECIES = 32,           /* SpeciesObservation column     */
+    MBOTS_EXPORT_PREV_SPECIES = 33       /* PrevSpeciesObservation column */
+};
+
+/* element types (madrona::py::TensorElementType subset) */
+enum mbots_dtype {
+    MBOTS_DTYPE_UINT8 = 0,
+    MBOTS_DTYPE_INT8 = 1,
+    MBOTS_DTYPE_INT32 = 2,
+    MBOTS_DTYPE_FLOAT32 = 3
+};
+
+/* A non-owning 2-D device tensor view (madrona::py::Tensor, mgr.cpp:138-144). */
+typedef struct mbots_tensor {
+    void   *data;        /* device pointer                                  */
+    int32_t dtype;       /* enum mbots_dtype                                */
+    int32_t device;      /* HIP device ordinal (gpuID)                      */
+    int64_t dims[2];     /* rows, columns                                   */
+} mbots_tensor;
+
+typedef struct mbots_handle mbots_handle;
+
+/* Manager::Manager / Impl::make (mgr.cpp:166-251).  Runs world init
+ * (Sim::Sim, sim.cpp:1232-1256) and the Init graph (sim.cpp:1050-1059). */
+int mbots_create(const mbots_config *cfg, mbots_handle **out);
+/* Manager::~Manager (mgr.cpp:253-255) */
+int mbots_destroy(mbots_handle *h);
+
+/* Manager::step (mgr.cpp:51-63, :257-260): Step + Sensor graphs, enqueued on
+ * `stream`.  Unlike the reference it does not block; mbots_num_agents and the
+ * host-side offsets synchronise with the last step on demand. */
+int mbots_step(mbots_handle *h, void *stream);
+/* Manager::shiftObservations (mgr.cpp:65-68, :262-265) */
+int mbots_shift_observations(mbots_handle *h, void *stream);
+
+/* SimBridge::totalNumAgents (sim.hpp:74-78, sim.cpp:992-993).  Waits for the
+ * last step's counters. */
+int mbots_num_agents(mbots_handle *h, uint32_t *out);
+/* Manager::exportTensor / the 11 tensor accessors (mgr.cpp:70-76, :267-490) */
+int mbots_export(mbots_handle *h, int32_t export_id, mbots_tensor *out);
+/* Manager::setAction (mgr.cpp:319-340): row = export row (species-major). */
+int mbots_set_action(mbots_handle *h, uint32_t row, const int32_t action[6]);
+/* Manager::agentOffsetForWorld (mgr.cpp:342-345) */
+int mbots_agent_offset_for_world(mbots_handle *h, uint32_t world, uint32_t *out);
+
+/* Build utilities (benchmark / test harness, not reference API):
+ * identity-keyed synthetic action stream: one-hot(threefry(seed,step |
+ * global_world, slot) % 6) written into the Action column of every live agent;
+ * hidden state gets hash-derived floats when write_hidden != 0. */
+int mbots_write_synthetic_actions(mbots_handle *h, uint32_t seed, uint32_t step,
+                                  int32_t write_hidden, void *stream);
+/* running total of agent-steps (sum over steps of live agents after the step) */
+int mbots_agent_steps(mbots_handle *h, uint64_t *out);
+/* births/respawns dropped because a world reached agent_capacity */
+int mbots_overflow(mbots_handle *h, uint64_t *out);
+/* Per-kernel device timing (bench.py roofline): when enabled, HIP events are
+ * recorded on the launch stream around every kernel; mbots_kernel_times
+ * synchronises and returns the summed milliseconds per kernel class
+ * (index = enum mbots_timed_kernel) and the number of launches of each. */
+enum mbots_timed_kernel {
+    MBOTS_TK_WORLD_STEP = 0, MBOTS_TK_SCAN = 1, MBOTS_TK_EXPORT = 2,
+    MBOTS_TK_SENSOR = 3, MBOTS_TK_SHIFT = 4, MBOTS_TK_ACTIONS = 5, MBOTS_TK_COUNT = 6
+};
+int mbots_enable_kernel_timing(mbots_handle *h, int32_t enable);
+int mbots_kernel_times(mbots_handle *h, double ms[MBOTS_TK_COUNT],
+                       uint64_t launches[MBOTS_TK_COUNT]);
+
+const char *mbots_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

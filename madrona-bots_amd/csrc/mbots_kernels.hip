@@ -1,0 +1,799 @@
+// mbots_kernels.hip -- hand-written gfx950 kernels of the per-step ECS sweep.
+//
+// Layout: agent state is SoA, [world][slot] with a
+// per-world slot capacity `cap`; one wave64 owns one world for the ECS
+// systems (4 worlds per 256-thread workgroup, no cross-wave sync), staging the
+// world's agents, chunk counters and food packages in LDS.  The exported
+// observation table is species-major (species, world, slot) and is written
+// into the other half of a double-buffered table every step.
+#include "mbots_kernels.hpp"
+
+namespace mbots {
+
+// ---------------------------------------------------------------------------
+// Per-world LDS image used by the world-step kernel
+// ---------------------------------------------------------------------------
+struct WorldLDS {
+    float x[kMaxCap], y[kMaxCap], rw[kMaxCap], rz[kMaxCap];
+    int32_t species[kMaxCap], accum[kMaxCap], finder[kMaxCap], obsrow[kMaxCap];
+    int32_t key[kMaxCap], take[kMaxCap];
+    uint32_t flags[kMaxCap];
+    float sur0[kMaxCap], sur1[kMaxCap];
+    uint32_t food[kNumPkg];
+    uint32_t nag[kNumChunks], spd[kNumChunks];
+    uint32_t cnt[kNumSpecies], hsum[kNumSpecies];
+    int32_t need[kNumSpecies];
+    int32_t scount[kNumSpecies];
+    int32_t consumed;
+};
+
+// flags bits
+constexpr uint32_t F_HIT_FRIENDLY = 1u << 0;
+constexpr uint32_t F_HIT_ENEMY = 1u << 1;
+constexpr uint32_t F_ATE = 1u << 2;
+constexpr uint32_t F_REPRO = 1u << 3;
+constexpr uint32_t F_ALIVE = 1u << 4;
+constexpr uint32_t F_BREED = 1u << 5;
+constexpr uint32_t F_STATS = 0xFu;
+
+constexpr int kWorldsPerBlock = 4;
+
+__device__ __forceinline__ uint32_t rng_draw(uint2 key, uint32_t ctr)
+{
+    return threefry2x32(key.x, key.y, ctr, 0u).x;
+}
+
+__device__ __forceinline__ void init_slot(WorldLDS &L, int s, float x, float y, int32_t sp,
+                                          int32_t h)
+{
+    L.x[s] = x;
+    L.y[s] = y;
+    L.rw[s] = 1.0f;
+    L.rz[s] = 0.0f;
+    L.species[s] = sp;
+    L.accum[s] = h;
+    L.finder[s] = -1;
+    L.obsrow[s] = -1;
+    L.flags[s] = F_ALIVE;
+    L.sur0[s] = 0.0f;
+    L.sur1[s] = 0.0f;
+}
+
+// ---------------------------------------------------------------------------
+// K1: world step -- resetChunkInfoSystem, addFoodSystem, actionSystem,
+// healthSync, updateSurroundingObservation, speciesTrackerUpdate,
+// speciesInfoSync + respawn, and the per-world compaction of
+// SortArchetypeNode<Agent, WorldID> (sim.cpp:1061-1132).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void world_step_kernel(SimState S, ObsTable cur)
+{
+    __shared__ WorldLDS lds[kWorldsPerBlock];
+    const uint32_t wv = threadIdx.x >> 6;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t w = blockIdx.x * kWorldsPerBlock + wv;
+    if (w >= S.W) return;
+    WorldLDS &L = lds[wv];
+    const uint32_t cap = S.cap;
+    const size_t base = (size_t)w * cap;
+    const int n0 = S.n[w];
+
+    // ---- stage the world in LDS ----
+    for (int i = lane; i < n0; i += 64) {
+        L.x[i] = S.x[base + i];
+        L.y[i] = S.y[base + i];
+        L.rw[i] = S.rw[base + i];
+        L.rz[i] = S.rz[base + i];
+        L.species[i] = S.species[base + i];
+        L.accum[i] = S.health[base + i];
+        L.finder[i] = S.finder[base + i];
+        L.obsrow[i] = S.obsrow[base + i];
+        L.flags[i] = F_ALIVE;
+    }
+    for (int k = lane; k < kNumPkg; k += 64) L.food[k] = S.food[(size_t)w * kNumPkg + k];
+    if (lane < kNumChunks) { L.nag[lane] = 0u; L.spd[lane] = 0u; }   // resetChunkInfoSystem
+    if (lane < kNumSpecies) { L.cnt[lane] = 0u; L.hsum[lane] = 0u; L.scount[lane] = 0; }
+    if (lane == 0) L.consumed = 0;
+    const uint2 key = S.key[w];
+    uint32_t ctr = S.ctr[w];
+    int32_t cur_food = S.cur_food[w];
+    wave_sync();
+
+    // ---- addFoodSystem (sim.cpp:363-387) + addFoodToChunk (:308-361), serial ----
+    if (lane == 0) {
+        if (sample_i32(rng_draw(key, ctr++), 0, 10) == 0) {
+            uint32_t nf = (uint32_t)sample_i32(rng_draw(key, ctr++), 1, 3);
+            uint32_t diff = (uint32_t)kFoodCap - (uint32_t)cur_food;
+            if (diff < nf) nf = diff;
+            for (uint32_t f = 0; f < nf; ++f) {
+                uint32_t cx = (uint32_t)sample_i32(rng_draw(key, ctr++), 0, kChunksX);
+                uint32_t cy = (uint32_t)sample_i32(rng_draw(key, ctr++), 0, kChunksY);
+                int chunk = (int)(cx + cy * kChunksX);
+                ctr += 2;   // two unused draws (sim.cpp:311-312)
+                for (int k = 0; k < kMaxPkg; ++k) {
+                    uint32_t p = L.food[chunk * kMaxPkg + k];
+                    if ((p >> 16) == 0u) {
+                        uint32_t rx = (uint32_t)sample_i32(rng_draw(key, ctr++), 0, kChunkW);
+                        uint32_t ry = (uint32_t)sample_i32(rng_draw(key, ctr++), 0, kChunkW);
+                        L.food[chunk * kMaxPkg + k] = (rx & 0xFFu) | ((ry & 0xFFu) << 8) | (1u << 16);
+                        ctr += 1;   // food entity rotation draw (sim.cpp:338-341)
+                        cur_food += 1;
+                        break;
+                    }
+                }
+            }
+        }
+    }
+    ctr = __shfl(ctr, 0);
+    cur_food = __shfl(cur_food, 0);
+    wave_sync();
+
+    // ---- actionSystem (sim.cpp:419-502) ----
+    for (int i = lane; i < n0; i += 64) {
+        int32_t act[6] = {0, 0, 0, 0, 0, 0};
+        const int32_t row = L.obsrow[i];
+        if (row >= 0) {
+            const int2 *ap = reinterpret_cast<const int2 *>(cur.action + (size_t)row * 6);
+            int2 a0 = ap[0], a1 = ap[1], a2 = ap[2];
+            act[0] = a0.x; act[1] = a0.y; act[2] = a1.x; act[3] = a1.y; act[4] = a2.x; act[5] = a2.y;
+        }
+        const int32_t sp = L.species[i];
+        uint32_t fl = F_ALIVE | (act[5] ? F_BREED : 0u);
+        const int32_t tgt = L.finder[i];
+        if (act[4] && tgt >= 0) {
+            atomicAdd(&L.accum[tgt], -50);
+            fl |= (L.species[tgt] == sp) ? F_HIT_FRIENDLY : F_HIT_ENEMY;
+        }
+        float rw = L.rw[i], rz = L.rz[i];
+        if (act[2]) {
+            float nw = rw * kRotC - rz * kRotS;
+            float nz = rw * kRotS + rz * kRotC;
+            rw = nw; rz = nz;
+        } else if (act[3]) {
+            float nw = rw * kRotC - rz * (-kRotS);
+            float nz = rw * (-kRotS) + rz * kRotC;
+            rw = nw; rz = nz;
+        }
+        float x = L.x[i], y = L.y[i];
+        const float ox = x, oy = y;
+        float dx, dy;
+        heading(rw, rz, dx, dy);
+        if (act[0]) { x = x + dx; y = y + dy; }
+        else if (act[1]) { x = x - dx; y = y - dy; }
+        x = fmin_std(kLx - 1.0f, fmax_std(0.0f, x));
+        y = fmin_std(kLy - 1.0f, fmax_std(0.0f, y));
+        float ddx = x - ox, ddy = y - oy;
+        float len = sqrtf(ddx * ddx + ddy * ddy);
+        int32_t ci = chunk_index(floorf((x / 1.0f) / 16.0f), floorf((y / 1.0f) / 16.0f));
+        atomicAdd(&L.nag[ci], 1u);
+        atomicAdd(&L.spd[ci], (uint32_t)(len * 2.0f));
+        L.x[i] = x; L.y[i] = y; L.rw[i] = rw; L.rz[i] = rz;
+        L.flags[i] = fl;
+    }
+    wave_sync();
+
+    // ---- healthSync (sim.cpp:505-581) ----
+    // food: the k-th agent (slot order) standing on a cell takes the k-th live
+    // package of that cell (serial consume() order made deterministic).
+    for (int i = lane; i < n0; i += 64) {
+        float chx = (L.x[i] / 1.0f) / 16.0f, chy = (L.y[i] / 1.0f) / 16.0f;
+        uint32_t cx = (uint8_t)(16.0f * (chx - floorf(chx)));
+        uint32_t cy = (uint8_t)(16.0f * (chy - floorf(chy)));
+        int32_t ci = chunk_index(chx, chy);
+        L.key[i] = (ci << 8) | (int32_t)(cy << 4) | (int32_t)cx;
+    }
+    wave_sync();
+    for (int i = lane; i < n0; i += 64) {
+        const int32_t kk = L.key[i];
+        const int ci = kk >> 8;
+        const uint32_t cx = (uint32_t)kk & 15u, cy = ((uint32_t)kk >> 4) & 15u;
+        int navail = 0;
+        for (int k = 0; k < kMaxPkg; ++k) {
+            uint32_t p = L.food[ci * kMaxPkg + k];
+            navail += ((p & 0xFFu) == cx && ((p >> 8) & 0xFFu) == cy && (p >> 16) != 0u) ? 1 : 0;
+        }
+        int take = -1;
+        if (navail > 0) {
+            int rank = 0;
+            for (int j = 0; j < i; ++j) rank += (L.key[j] == kk) ? 1 : 0;
+            if (rank < navail) {
+                for (int k = 0; k < kMaxPkg; ++k) {
+                    uint32_t p = L.food[ci * kMaxPkg + k];
+                    if ((p & 0xFFu) == cx && ((p >> 8) & 0xFFu) == cy && (p >> 16) != 0u) {
+                        if (rank == 0) { take = ci * kMaxPkg + k; break; }
+                        --rank;
+                    }
+                }
+            }
+        }
+        L.take[i] = take;
+    }
+    wave_sync();
+    int n1 = n0;
+    uint32_t ovf = 0;
+    for (int b = 0; b < n0; b += 64) {
+        const int i = b + (int)lane;
+        const bool active = i < n0;
+        bool want_child = false;
+        if (active) {
+            int32_t h = L.accum[i];
+            uint32_t fl = L.flags[i];
+            const int take = L.take[i];
+            if (take >= 0) {
+                L.food[take] &= 0xFFFFu;   // numFood 1 -> 0
+                atomicAdd(&L.consumed, 1);
+                h = (int32_t)((float)h + 20.0f);
+                fl |= F_ATE;
+            }
+            const int32_t tgt = L.finder[i];
+            if ((fl & F_BREED) && h > 10 && tgt >= 0) {
+                if (L.species[tgt] == L.species[i]) {
+                    h -= 40;
+                    fl |= F_REPRO;
+                    want_child = true;
+                }
+            }
+            if (h <= 0) fl &= ~F_ALIVE;
+            L.accum[i] = h;
+            L.flags[i] = fl;
+        }
+        const uint64_t m = ballot64(want_child);
+        if (want_child) {
+            const int s = n1 + (int)rank_below(m);
+            if (s < (int)cap) init_slot(L, s, L.x[i], L.y[i], L.species[i], 50);
+        }
+        const int made = __popcll(m);
+        const int room = (int)cap - n1;
+        if (made > room) { ovf += (uint32_t)(made - room); n1 = (int)cap; }
+        else n1 += made;
+    }
+    wave_sync();
+    cur_food -= L.consumed;
+
+    // ---- updateSurroundingObservation (sim.cpp:583-654) + tracker (:719-734) ----
+    for (int i = lane; i < n1; i += 64) {
+        if (!(L.flags[i] & F_ALIVE)) continue;
+        float cpx = L.x[i] / 1.0f, cpy = L.y[i] / 1.0f;
+        cpx = cpx - 16.0f * 0.5f;
+        cpy = cpy - 16.0f * 0.5f;
+        float chx = cpx / 16.0f, chy = cpy / 16.0f;
+        float x0 = floorf(chx), y0 = floorf(chy), x1 = ceilf(chx), y1 = ceilf(chy);
+        int32_t i00 = chunk_index(x0, y0), i10 = chunk_index(x1, y0);
+        int32_t i01 = chunk_index(x0, y1), i11 = chunk_index(x1, y1);
+        float xi = chx - x0, yi = chy - y0;
+        float n00 = i00 >= 0 ? (float)L.nag[i00] : 0.0f;
+        float n10 = i10 >= 0 ? (float)L.nag[i10] : 0.0f;
+        float n01 = i01 >= 0 ? (float)L.nag[i01] : 0.0f;
+        float n11 = i11 >= 0 ? (float)L.nag[i11] : 0.0f;
+        float s00 = i00 >= 0 ? (float)L.spd[i00] : 0.0f;
+        float s10 = i10 >= 0 ? (float)L.spd[i10] : 0.0f;
+        float s01 = i01 >= 0 ? (float)L.spd[i01] : 0.0f;
+        float s11 = i11 >= 0 ? (float)L.spd[i11] : 0.0f;
+        float nx0 = xi * n10 + (1.0f - xi) * n00;
+        float nx1 = xi * n11 + (1.0f - xi) * n01;
+        float sx0 = xi * s10 + (1.0f - xi) * s00;
+        float sx1 = xi * s11 + (1.0f - xi) * s01;
+        L.sur0[i] = yi * nx1 + (1.0f - yi) * nx0;
+        L.sur1[i] = yi * sx1 + (1.0f - yi) * sx0;
+        const int sp = L.species[i] - 1;
+        atomicAdd(&L.cnt[sp], 1u);
+        atomicAdd(&L.hsum[sp], (uint32_t)L.accum[i]);
+    }
+    wave_sync();
+
+    // ---- speciesInfoSync (sim.cpp:791-838) ----
+    const int A = (int)S.A;
+    const uint32_t per_species = S.A / kNumSpecies;
+    if (lane < kNumSpecies) {
+        const uint32_t count = L.cnt[lane];
+        float avg = (float)L.hsum[lane] / (float)count;
+        if (count == 0) avg = 0.0f;
+        S.sreward[(size_t)w * kNumSpecies + lane] = (float)count / (float)A + avg / 100.0f - 2.0f;
+        L.need[lane] = count < per_species ? (int32_t)(per_species - count) : 0;
+    }
+    wave_sync();
+    const int need0 = L.need[0], need1 = L.need[1], need2 = L.need[2], need3 = L.need[3];
+    const int total_need = need0 + need1 + need2 + need3;
+    for (int k = lane; k < total_need; k += 64) {
+        int sp = k < need0 ? 1 : (k < need0 + need1 ? 2 : (k < need0 + need1 + need2 ? 3 : 4));
+        float x = u01(rng_draw(key, ctr + 2u * (uint32_t)k)) * kLx;
+        float y = u01(rng_draw(key, ctr + 2u * (uint32_t)k + 1u)) * kLy;
+        const int s = n1 + k;
+        if (s < (int)cap) init_slot(L, s, x, y, sp, 100);
+    }
+    ctr += 2u * (uint32_t)total_need;
+    int n2 = n1 + total_need;
+    if (n2 > (int)cap) { ovf += (uint32_t)(n2 - (int)cap); n2 = (int)cap; }
+    wave_sync();
+
+    // ---- compaction (SortArchetypeNode<Agent, WorldID>, sim.cpp:1129) ----
+    int nn = 0;
+    for (int b = 0; b < n2; b += 64) {
+        const int i = b + (int)lane;
+        const bool alive = i < n2 && (L.flags[i] & F_ALIVE);
+        const uint64_t m = ballot64(alive);
+        if (alive) {
+            const size_t d = base + nn + rank_below(m);
+            S.x[d] = L.x[i];
+            S.y[d] = L.y[i];
+            S.rw[d] = L.rw[i];
+            S.rz[d] = L.rz[i];
+            S.species[d] = L.species[i];
+            S.health[d] = L.accum[i];
+            S.obsrow[d] = L.obsrow[i];
+            S.sur0[d] = L.sur0[i];
+            S.sur1[d] = L.sur1[i];
+            S.stats[d] = L.flags[i] & F_STATS;
+            atomicAdd(&L.scount[L.species[i] - 1], 1);
+        }
+        nn += __popcll(m);
+    }
+    for (int k = lane; k < kNumPkg; k += 64) S.food[(size_t)w * kNumPkg + k] = L.food[k];
+    wave_sync();
+    if (lane < kNumSpecies) S.scount[(size_t)w * kNumSpecies + lane] = L.scount[lane];
+    if (lane == 0) {
+        S.n[w] = nn;
+        S.ctr[w] = ctr;
+        S.cur_food[w] = cur_food;
+        if (ovf) S.overflow[w] += ovf;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// K2: species-major row offsets.  row_base[w][s] = sum_{s'<s} total[s'] +
+// sum_{w'<w} count[w'][s]  (SortArchetypeNode<Obs, SpeciesObservation>,
+// sim.cpp:1147-1149, made deterministic); world_off[w] for agentOffsetForWorld.
+// One 1024-thread workgroup.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(1024) void scan_kernel(SimState S)
+{
+    constexpr int T = 1024;
+    __shared__ int32_t sh[5][T];
+    __shared__ int32_t tot[5];
+    const int t = threadIdx.x;
+    const int W = (int)S.W;
+    const int per = (W + T - 1) / T;
+    const int w0 = t * per, w1 = min(W, w0 + per);
+    int32_t loc[5] = {0, 0, 0, 0, 0};
+    for (int w = w0; w < w1; ++w) {
+        const int4 c = reinterpret_cast<const int4 *>(S.scount)[w];
+        loc[0] += c.x; loc[1] += c.y; loc[2] += c.z; loc[3] += c.w;
+        loc[4] += S.n[w];
+    }
+    for (int k = 0; k < 5; ++k) sh[k][t] = loc[k];
+    __syncthreads();
+    // Hillis-Steele inclusive scan over the 1024 partial sums
+    for (int off = 1; off < T; off <<= 1) {
+        int32_t v[5];
+        for (int k = 0; k < 5; ++k) v[k] = (t >= off) ? sh[k][t - off] : 0;
+        __syncthreads();
+        for (int k = 0; k < 5; ++k) sh[k][t] += v[k];
+        __syncthreads();
+    }
+    if (t == T - 1) for (int k = 0; k < 5; ++k) tot[k] = sh[k][t];
+    __syncthreads();
+    int32_t run[5];
+    for (int k = 0; k < 5; ++k) run[k] = sh[k][t] - loc[k];
+    const int32_t sb0 = 0, sb1 = tot[0], sb2 = tot[0] + tot[1], sb3 = tot[0] + tot[1] + tot[2];
+    for (int w = w0; w < w1; ++w) {
+        const int4 c = reinterpret_cast<const int4 *>(S.scount)[w];
+        int4 rb;
+        rb.x = sb0 + run[0]; rb.y = sb1 + run[1]; rb.z = sb2 + run[2]; rb.w = sb3 + run[3];
+        reinterpret_cast<int4 *>(S.row_base)[w] = rb;
+        S.world_off[w] = run[4];
+        run[0] += c.x; run[1] += c.y; run[2] += c.z; run[3] += c.w;
+        run[4] += S.n[w];
+    }
+    if (t == 0) {
+        S.totals[0] = (uint32_t)tot[4];
+        for (int k = 0; k < 4; ++k) S.totals[1 + k] = (uint32_t)tot[k];
+        *S.agent_steps += (unsigned long long)tot[4];
+    }
+}
+
+// ---------------------------------------------------------------------------
+// K3: export -- updateObservations (sim.cpp:687-717), the species-major row
+// move, updateSensorOutputIdx (:736-789) and rewardSystem setting 8
+// (:840-983).  One wave per world writes its agents' rows into `nxt`,
+// carrying Action/HiddenState/Prev* from the old row in `cur`.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void export_kernel(SimState S, ObsTable cur, ObsTable nxt,
+                                                     int init)
+{
+    const uint32_t wv = threadIdx.x >> 6;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t w = blockIdx.x * kWorldsPerBlock + wv;
+    if (w >= S.W) return;
+    const size_t base = (size_t)w * S.cap;
+    const int n = S.n[w];
+    const int4 rb = reinterpret_cast<const int4 *>(S.row_base)[w];
+    const float4 rew = reinterpret_cast<const float4 *>(S.sreward)[w];
+    const bool fixed = (S.flags & kFlagRewardFixed) != 0;
+    const bool depth = (S.flags & kFlagFixDepth) != 0;
+    // faithful B.3: rewards[4] reads the next SpeciesInfo row's rewards[0]
+    const float next_r0 = (w + 1 < S.W) ? S.sreward[(size_t)(w + 1) * kNumSpecies] : 0.0f;
+    int carry0 = 0, carry1 = 0, carry2 = 0, carry3 = 0;
+    for (int b = 0; b < n; b += 64) {
+        const int i = b + (int)lane;
+        const bool active = i < n;
+        const int32_t sp = active ? S.species[base + i] : 0;
+        const uint64_t m1 = ballot64(sp == 1), m2 = ballot64(sp == 2);
+        const uint64_t m3 = ballot64(sp == 3), m4 = ballot64(sp == 4);
+        int32_t row = 0;
+        if (sp == 1) row = rb.x + carry0 + (int32_t)rank_below(m1);
+        else if (sp == 2) row = rb.y + carry1 + (int32_t)rank_below(m2);
+        else if (sp == 3) row = rb.z + carry2 + (int32_t)rank_below(m3);
+        else if (sp == 4) row = rb.w + carry3 + (int32_t)rank_below(m4);
+        carry0 += __popcll(m1); carry1 += __popcll(m2);
+        carry2 += __popcll(m3); carry3 += __popcll(m4);
+        if (!active) continue;
+
+        const size_t r = (size_t)row;
+        const float x = S.x[base + i], y = S.y[base + i];
+        const int32_t h = S.health[base + i];
+        const float s0 = init ? 0.0f : S.sur0[base + i];
+        const float s1 = init ? 0.0f : S.sur1[base + i];
+        const uint32_t st = init ? 0u : S.stats[base + i];
+        const int32_t orow = S.obsrow[base + i];
+
+        nxt.species[r] = sp;
+        reinterpret_cast<float2 *>(nxt.pos)[r] = make_float2(x, y);
+        nxt.health[r] = h;
+        reinterpret_cast<float2 *>(nxt.sur)[r] = make_float2(s0, s1);
+        const int4 stv = make_int4((int)(st & 1u), (int)((st >> 1) & 1u), (int)((st >> 2) & 1u),
+                                   (int)((st >> 3) & 1u));
+        reinterpret_cast<int4 *>(nxt.stats)[r] = stv;
+
+        // rewardSystem, setting 8 (sim.cpp:942-956)
+        float rv = 0.0f;
+        if (!init) {
+            float sr;
+            if (fixed) sr = sp == 1 ? rew.x : sp == 2 ? rew.y : sp == 3 ? rew.z : rew.w;
+            else sr = sp == 1 ? rew.y : sp == 2 ? rew.z : sp == 3 ? rew.w : next_r0;
+            rv = sr + (float)h / 100.0f - 0.5f;
+            if (stv.z) rv += 10.0f;
+            if (stv.w) rv += 10.0f;
+            if (stv.y) rv += 15.0f;
+        }
+        nxt.reward[r] = rv;
+
+        int2 a0 = make_int2(0, 0), a1 = a0, a2 = a0, pa0 = a0, pa1 = a0, pa2 = a0;
+        float4 h0 = make_float4(0.f, 0.f, 0.f, 0.f), h1 = h0, h2 = h0, h3 = h0;
+        float4 q0 = h0, q1 = h0, q2 = h0, q3 = h0;
+        int32_t psp = 0, ph = 0;
+        float2 ppos = make_float2(0.f, 0.f), psur = ppos;
+        float prew = 0.0f;
+        int4 pst = make_int4(0, 0, 0, 0);
+        uint4 sem0 = make_uint4(0u, 0u, 0u, 0u), sem1 = sem0, dep0 = sem0, dep1 = sem0;
+        if (orow >= 0) {
+            const size_t o = (size_t)orow;
+            const int2 *ap = reinterpret_cast<const int2 *>(cur.action + o * 6);
+            a0 = ap[0]; a1 = ap[1]; a2 = ap[2];
+            const float4 *hp = reinterpret_cast<const float4 *>(cur.hidden + o * kHidden);
+            h0 = hp[0]; h1 = hp[1]; h2 = hp[2]; h3 = hp[3];
+            psp = cur.pspecies[o];
+            ppos = reinterpret_cast<const float2 *>(cur.ppos)[o];
+            ph = cur.phealth[o];
+            psur = reinterpret_cast<const float2 *>(cur.psur)[o];
+            prew = cur.preward[o];
+            const int2 *pap = reinterpret_cast<const int2 *>(cur.paction + o * 6);
+            pa0 = pap[0]; pa1 = pap[1]; pa2 = pap[2];
+            pst = reinterpret_cast<const int4 *>(cur.pstats)[o];
+            const float4 *php = reinterpret_cast<const float4 *>(cur.phidden + o * kHidden);
+            q0 = php[0]; q1 = php[1]; q2 = php[2]; q3 = php[3];
+            const uint4 *sp4 = reinterpret_cast<const uint4 *>(cur.sem + o * kSensor);
+            sem0 = sp4[0]; sem1 = sp4[1];
+            if (depth) {
+                const uint4 *dp4 = reinterpret_cast<const uint4 *>(cur.depth + o * kSensor);
+                dep0 = dp4[0]; dep1 = dp4[1];
+            }
+        }
+        int2 *nap = reinterpret_cast<int2 *>(nxt.action + r * 6);
+        nap[0] = a0; nap[1] = a1; nap[2] = a2;
+        float4 *nhp = reinterpret_cast<float4 *>(nxt.hidden + r * kHidden);
+        nhp[0] = h0; nhp[1] = h1; nhp[2] = h2; nhp[3] = h3;
+        nxt.pspecies[r] = psp;
+        reinterpret_cast<float2 *>(nxt.ppos)[r] = ppos;
+        nxt.phealth[r] = ph;
+        reinterpret_cast<float2 *>(nxt.psur)[r] = psur;
+        nxt.preward[r] = prew;
+        int2 *npap = reinterpret_cast<int2 *>(nxt.paction + r * 6);
+        npap[0] = pa0; npap[1] = pa1; npap[2] = pa2;
+        reinterpret_cast<int4 *>(nxt.pstats)[r] = pst;
+        float4 *nphp = reinterpret_cast<float4 *>(nxt.phidden + r * kHidden);
+        nphp[0] = q0; nphp[1] = q1; nphp[2] = q2; nphp[3] = q3;
+        uint4 *nps = reinterpret_cast<uint4 *>(nxt.psem + r * kSensor);
+        nps[0] = sem0; nps[1] = sem1;
+        if (depth) {
+            uint4 *npd = reinterpret_cast<uint4 *>(nxt.pdepth + r * kSensor);
+            npd[0] = dep0; npd[1] = dep1;
+        }
+        S.obsrow[base + i] = row;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// K4: sensor -- 32-pixel raycast (24 forward + 8 backward) plus the finder ray
+// (Madrona RenderingSystem, sim.cpp:1183-1188; spec DESIGN.md 3.6).
+// One wave per world; lanes sweep (agent, ray) pairs; objects staged in LDS.
+// ---------------------------------------------------------------------------
+struct SensorLDS {
+    float ax[kMaxCap], ay[kMaxCap], dx[kMaxCap], dy[kMaxCap];
+    int32_t sp[kMaxCap];
+    float fx[kNumPkg], fy[kNumPkg];
+    int8_t sem[kMaxCap * kSensor];
+    uint8_t dep[kMaxCap * kSensor];
+    int32_t nfood;
+};
+
+__constant__ float kWallBox[4][4] = {
+    {64.0f - 64.0f, 64.0f + 64.0f, 0.0f - 0.2f, 0.0f + 0.2f},
+    {0.0f - 0.2f, 0.0f + 0.2f, 48.0f - 48.0f, 48.0f + 48.0f},
+    {64.0f - 64.0f, 64.0f + 64.0f, 96.0f - 0.2f, 96.0f + 0.2f},
+    {128.0f - 0.2f, 128.0f + 0.2f, 48.0f - 48.0f, 48.0f + 48.0f},
+};
+
+__global__ __launch_bounds__(256) void sensor_kernel(SimState S, ObsTable nxt)
+{
+    __shared__ SensorLDS lds[kWorldsPerBlock];
+    const uint32_t wv = threadIdx.x >> 6;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t w = blockIdx.x * kWorldsPerBlock + wv;
+    if (w >= S.W) return;
+    SensorLDS &L = lds[wv];
+    const size_t base = (size_t)w * S.cap;
+    const int n = S.n[w];
+    const bool depth = (S.flags & kFlagFixDepth) != 0;
+    for (int i = lane; i < n; i += 64) {
+        L.ax[i] = S.x[base + i];
+        L.ay[i] = S.y[base + i];
+        L.sp[i] = S.species[base + i];
+        float dx, dy;
+        heading(S.rw[base + i], S.rz[base + i], dx, dy);
+        L.dx[i] = dx;
+        L.dy[i] = dy;
+    }
+    // live food packages in (chunk, package) order
+    int nf = 0;
+    for (int b = 0; b < kNumPkg; b += 64) {
+        const int k = b + (int)lane;
+        uint32_t p = k < kNumPkg ? S.food[(size_t)w * kNumPkg + k] : 0u;
+        const bool live = (p >> 16) != 0u;
+        const uint64_t m = ballot64(live);
+        if (live) {
+            const int c = k / kMaxPkg;
+            const float bx = (float)((c % kChunksX) * kChunkW);
+            const float by = (float)((c / kChunksX) * kChunkW);
+            const int s = nf + (int)rank_below(m);
+            L.fx[s] = (float)(p & 0xFFu) + bx;
+            L.fy[s] = (float)((p >> 8) & 0xFFu) + by;
+        }
+        nf += __popcll(m);
+    }
+    wave_sync();
+    const int npairs = n * kRays;
+    for (int p = lane; p < npairs; p += 64) {
+        const int i = p / kRays, ray = p - i * kRays;
+        const float ox = L.ax[i], oy = L.ay[i], hx = L.dx[i], hy = L.dy[i];
+        const float rx = hy, ry = -hx;
+        float dx, dy;
+        if (ray < 24) {
+            const float u = (float)(2 * ray + 1) / 24.0f - 1.0f;
+            dx = hx + u * rx;
+            dy = hy + u * ry;
+        } else if (ray < kSensor) {
+            const float u = (float)(2 * (ray - 24) + 1) / 8.0f - 1.0f;
+            dx = -(hx + u * rx);
+            dy = -(hy + u * ry);
+        } else {
+            dx = hx;
+            dy = hy;
+        }
+        float best = __builtin_inff(), t;
+        int sem = -1, slot = -1;
+        for (int k = 0; k < 4; ++k) {
+            if (ray_box(ox, oy, dx, dy, kWallBox[k][0], kWallBox[k][1], kWallBox[k][2],
+                        kWallBox[k][3], t) && t < best) {
+                best = t; sem = 5; slot = -1;
+            }
+        }
+        for (int f = 0; f < nf; ++f) {
+            const float fx = L.fx[f], fy = L.fy[f];
+            if (ray_box(ox, oy, dx, dy, fx - 1.0f, fx + 1.0f, fy - 1.0f, fy + 1.0f, t) &&
+                t < best) {
+                best = t; sem = 6; slot = -1;
+            }
+        }
+        for (int j = 0; j < n; ++j) {
+            if (j == i) continue;
+            if (ray_circle(ox, oy, dx, dy, L.ax[j], L.ay[j], t) && t < best) {
+                best = t; sem = L.sp[j]; slot = j;
+            }
+        }
+        if (ray < kSensor) {
+            L.sem[i * kSensor + ray] = (int8_t)sem;
+            if (depth) L.dep[i * kSensor + ray] = depth_u8(best);
+        } else {
+            S.finder[base + i] = slot;
+        }
+    }
+    wave_sync();
+    // rows out: two lanes per agent, 16 B each
+    for (int q = lane; q < 2 * n; q += 64) {
+        const int i = q >> 1, half = q & 1;
+        const size_t r = (size_t)S.obsrow[base + i];
+        const uint4 v = reinterpret_cast<const uint4 *>(L.sem + i * kSensor)[half];
+        reinterpret_cast<uint4 *>(nxt.sem + r * kSensor)[half] = v;
+        if (depth) {
+            const uint4 d = reinterpret_cast<const uint4 *>(L.dep + i * kSensor)[half];
+            reinterpret_cast<uint4 *>(nxt.depth + r * kSensor)[half] = d;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// shiftObservationsSystem + shiftHiddenState (sim.cpp:1002-1048): Prev* <-
+// current for rows [0, N), with the reference's prevStats.hitEnemyAgent =
+// stats.hitFriendlyAgent (sim.cpp:1034).  N is read on the device.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void shift_kernel(const uint32_t *totals, ObsTable t)
+{
+    const uint32_t N = totals[0];
+    const uint32_t stride = gridDim.x * blockDim.x;
+    for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r < N; r += stride) {
+        t.pspecies[r] = t.species[r];
+        reinterpret_cast<float2 *>(t.ppos)[r] = reinterpret_cast<const float2 *>(t.pos)[r];
+        t.phealth[r] = t.health[r];
+        reinterpret_cast<float2 *>(t.psur)[r] = reinterpret_cast<const float2 *>(t.sur)[r];
+        t.preward[r] = t.reward[r];
+        const int2 *a = reinterpret_cast<const int2 *>(t.action + (size_t)r * 6);
+        int2 *pa = reinterpret_cast<int2 *>(t.paction + (size_t)r * 6);
+        pa[0] = a[0]; pa[1] = a[1]; pa[2] = a[2];
+        int4 s = reinterpret_cast<const int4 *>(t.stats)[r];
+        s.y = s.x;
+        reinterpret_cast<int4 *>(t.pstats)[r] = s;
+        const float4 *h = reinterpret_cast<const float4 *>(t.hidden + (size_t)r * kHidden);
+        float4 *ph = reinterpret_cast<float4 *>(t.phidden + (size_t)r * kHidden);
+        ph[0] = h[0]; ph[1] = h[1]; ph[2] = h[2]; ph[3] = h[3];
+    }
+}
+
+// ---------------------------------------------------------------------------
+// World init: Sim::Sim + initWorld (sim.cpp:233-275, :1232-1256) and the Init
+// graph's initializeChunks (sim.cpp:277-300).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void init_kernel(SimState S)
+{
+    const uint32_t wv = threadIdx.x >> 6;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t w = blockIdx.x * kWorldsPerBlock + wv;
+    if (w >= S.W) return;
+    const size_t base = (size_t)w * S.cap;
+    const uint32_t gw = S.world_offset + w;
+    const uint2 key = threefry2x32(S.seed, 0u, 0u, gw);   // split_i(initKey(seed), 0, world)
+    const int A = (int)S.A;
+    for (int i = lane; i < A; i += 64) {
+        const float x = u01(rng_draw(key, 2u * (uint32_t)i)) * kLx;
+        const float y = u01(rng_draw(key, 2u * (uint32_t)i + 1u)) * kLy;
+        S.x[base + i] = x;
+        S.y[base + i] = y;
+        S.rw[base + i] = 1.0f;
+        S.rz[base + i] = 0.0f;
+        S.species[base + i] = (i % kNumSpecies) + 1;
+        S.health[base + i] = 100;
+        S.finder[base + i] = -1;
+        S.obsrow[base + i] = -1;
+        S.sur0[base + i] = 0.0f;
+        S.sur1[base + i] = 0.0f;
+        S.stats[base + i] = 0u;
+    }
+    for (int k = lane; k < kNumPkg; k += 64) S.food[(size_t)w * kNumPkg + k] = 0u;
+    if (lane < kNumSpecies) {
+        S.scount[(size_t)w * kNumSpecies + lane] = A / kNumSpecies + ((int)lane < A % kNumSpecies ? 1 : 0);
+        S.sreward[(size_t)w * kNumSpecies + lane] = 0.0f;
+    }
+    if (lane == 0) {
+        S.key[w] = key;
+        S.ctr[w] = 2u * (uint32_t)A;
+        S.n[w] = A;
+        S.cur_food[w] = 0;
+        S.overflow[w] = 0u;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Harness: identity-keyed synthetic action stream
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void synthetic_actions_kernel(SimState S, ObsTable t,
+                                                                uint32_t seed, uint32_t step,
+                                                                int write_hidden)
+{
+    const uint32_t wv = threadIdx.x >> 6;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t w = blockIdx.x * kWorldsPerBlock + wv;
+    if (w >= S.W) return;
+    const size_t base = (size_t)w * S.cap;
+    const uint32_t gw = S.world_offset + w;
+    const int n = S.n[w];
+    for (int i = lane; i < n; i += 64) {
+        const size_t r = (size_t)S.obsrow[base + i];
+        const uint32_t k = threefry2x32(seed, step, gw, (uint32_t)i).x % 6u;
+        int2 *ap = reinterpret_cast<int2 *>(t.action + r * 6);
+        ap[0] = make_int2(k == 0, k == 1);
+        ap[1] = make_int2(k == 2, k == 3);
+        ap[2] = make_int2(k == 4, k == 5);
+        if (write_hidden) {
+            for (int j = 0; j < kHidden; ++j) {
+                const uint32_t hb = threefry2x32(seed ^ 0x9E3779B9u, step, gw,
+                                                 (uint32_t)i * kHidden + (uint32_t)j).x;
+                t.hidden[r * kHidden + j] = u01(hb) - 0.5f;
+            }
+        }
+    }
+}
+
+// sensorIndexTensor (mgr.cpp:309-317): world-major agent order -> export row
+__global__ __launch_bounds__(256) void sensor_index_kernel(SimState S, int32_t *out)
+{
+    const uint32_t wv = threadIdx.x >> 6;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t w = blockIdx.x * kWorldsPerBlock + wv;
+    if (w >= S.W) return;
+    const size_t base = (size_t)w * S.cap;
+    const int n = S.n[w], off = S.world_off[w];
+    for (int i = lane; i < n; i += 64) out[off + i] = S.obsrow[base + i];
+}
+
+// ---------------------------------------------------------------------------
+// Host-side launchers
+// ---------------------------------------------------------------------------
+static inline unsigned world_blocks(uint32_t W) { return (W + kWorldsPerBlock - 1) / kWorldsPerBlock; }
+
+hipError_t launch_init(const SimState &S, hipStream_t st)
+{
+    hipLaunchKernelGGL(init_kernel, dim3(world_blocks(S.W)), dim3(256), 0, st, S);
+    return hipGetLastError();
+}
+hipError_t launch_world_step(const SimState &S, const ObsTable &cur, hipStream_t st)
+{
+    hipLaunchKernelGGL(world_step_kernel, dim3(world_blocks(S.W)), dim3(256), 0, st, S, cur);
+    return hipGetLastError();
+}
+hipError_t launch_scan(const SimState &S, hipStream_t st)
+{
+    hipLaunchKernelGGL(scan_kernel, dim3(1), dim3(1024), 0, st, S);
+    return hipGetLastError();
+}
+hipError_t launch_export(const SimState &S, const ObsTable &cur, const ObsTable &nxt, int init,
+                         hipStream_t st)
+{
+    hipLaunchKernelGGL(export_kernel, dim3(world_blocks(S.W)), dim3(256), 0, st, S, cur, nxt, init);
+    return hipGetLastError();
+}
+hipError_t launch_sensor(const SimState &S, const ObsTable &nxt, hipStream_t st)
+{
+    hipLaunchKernelGGL(sensor_kernel, dim3(world_blocks(S.W)), dim3(256), 0, st, S, nxt);
+    return hipGetLastError();
+}
+hipError_t launch_shift(const SimState &S, const ObsTable &t, hipStream_t st)
+{
+    unsigned rows = S.W * S.cap;
+    unsigned blocks = (rows + 255) / 256;
+    if (blocks > 4096) blocks = 4096;
+    if (blocks == 0) blocks = 1;
+    hipLaunchKernelGGL(shift_kernel, dim3(blocks), dim3(256), 0, st, S.totals, t);
+    return hipGetLastError();
+}
+hipError_t launch_synthetic_actions(const SimState &S, const ObsTable &t, uint32_t seed,
+                                    uint32_t step, int write_hidden, hipStream_t st)
+{
+    hipLaunchKernelGGL(synthetic_actions_kernel, dim3(world_blocks(S.W)), dim3(256), 0, st, S, t,
+                       seed, step, write_hidden);
+    return hipGetLastError();
+}
+hipError_t launch_sensor_index(const SimState &S, int32_t *out, hipStream_t st)
+{
+    hipLaunchKernelGGL(sensor_index_kernel, dim3(world_blocks(S.W)), dim3(256), 0, st, S, out);
+    return hipGetLastError();
+}
+
+}  // namespace mbots

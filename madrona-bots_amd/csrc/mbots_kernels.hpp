@@ -1,0 +1,55 @@
+// mbots_kernels.hpp -- device state descriptors and kernel launchers.
+#pragma once
+
+#include "mbots_device.hpp"
+
+namespace mbots {
+
+constexpr uint32_t kFlagRewardFixed = 0x1u;   // MBOTS_FLAG_REWARD_FIXED
+constexpr uint32_t kFlagFixDepth = 0x2u;      // MBOTS_FLAG_FIX_DEPTH_ALIAS
+
+// Agent / world state in HBM (SoA).  Agent columns are [W][cap].
+struct SimState {
+    float *x, *y, *rw, *rz;         // base::Position.xy, base::Rotation (w, z)
+    int32_t *species;               // Species
+    int32_t *health;                // Health (== HealthAccumulator between steps)
+    int32_t *finder;                // FinderOutput hit -> slot in the same world, -1 none
+    int32_t *obsrow;                // AgentObservationBridge -> export row
+    float *sur0, *sur1;             // SurroundingObservation (step-local)
+    uint32_t *stats;                // AgentStats bits (step-local)
+    int32_t *n;                     // [W] live agents per world
+    uint32_t *ctr;                  // [W] RNG counter
+    uint2 *key;                     // [W] RNG key
+    uint32_t *food;                 // [W][240] packed x | y << 8 | numFood << 16
+    int32_t *cur_food;              // [W] Sim::currentNumFood
+    float *sreward;                 // [W][4] SpeciesReward
+    int32_t *scount;                // [W][4] SpeciesCount (exported)
+    int32_t *row_base;              // [W][4] first export row of (world, species)
+    int32_t *world_off;             // [W] world-major agent offsets
+    uint32_t *overflow;             // [W] dropped births/respawns
+    uint32_t *totals;               // [0] = N, [1..4] = per-species rows
+    unsigned long long *agent_steps;
+    uint32_t W, cap, A, world_offset, flags, seed;
+};
+
+// One half of the double-buffered species-major observation table
+// (AgentObservationArchetype, types.hpp:228-252, + raycast output columns).
+struct ObsTable {
+    int32_t *species;  float *pos;  int32_t *health;  float *sur;  float *reward;
+    int32_t *action;   int32_t *stats;  float *hidden;  int8_t *sem;  uint8_t *depth;
+    int32_t *pspecies; float *ppos; int32_t *phealth; float *psur; float *preward;
+    int32_t *paction;  int32_t *pstats; float *phidden; int8_t *psem; uint8_t *pdepth;
+};
+
+hipError_t launch_init(const SimState &S, hipStream_t st);
+hipError_t launch_world_step(const SimState &S, const ObsTable &cur, hipStream_t st);
+hipError_t launch_scan(const SimState &S, hipStream_t st);
+hipError_t launch_export(const SimState &S, const ObsTable &cur, const ObsTable &nxt, int init,
+                         hipStream_t st);
+hipError_t launch_sensor(const SimState &S, const ObsTable &nxt, hipStream_t st);
+hipError_t launch_shift(const SimState &S, const ObsTable &t, hipStream_t st);
+hipError_t launch_synthetic_actions(const SimState &S, const ObsTable &t, uint32_t seed,
+                                    uint32_t step, int write_hidden, hipStream_t st);
+hipError_t launch_sensor_index(const SimState &S, int32_t *out, hipStream_t st);
+
+}  // namespace mbots

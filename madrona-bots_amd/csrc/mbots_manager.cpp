@@ -1,0 +1,470 @@
+// mbots_manager.cpp -- host orchestration (the reference's Manager,
+// src/entry/mgr.cpp) behind the C ABI declared in include/mbots.h.
+//
+// MI355X-first differences from the reference Manager:
+//  * no runtime compilation: kernels are ahead-of-time gfx950 code objects;
+//  * every launch goes on the caller's HIP stream (torch's current stream), and
+//    step() does not block -- the host-side agent count is fetched lazily by an
+//    async D2H copy into pinned memory plus an event (mgr.cpp:57-62 did two
+//    blocking cudaMemcpy per step);
+//  * all device memory is one arena sized for `num_worlds * agent_capacity`
+//    rows (288 GB HBM per GPU leaves ample headroom);
+//  * the species-major export table is double-buffered: a step writes the new
+//    table while reading the old one (no in-place radix sort of 264-B rows).
+#include "../../include/mbots.h"
+#include "mbots_kernels.hpp"
+
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string &msg)
+{
+    g_err = msg;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                      \
+    do {                                                                                   \
+        hipError_t _e = (expr);                                                            \
+        if (_e != hipSuccess)                                                              \
+            return fail(MBOTS_E_HIP, std::string(#expr) + ": " + hipGetErrorString(_e)); \
+    } while (0)
+
+struct Arena {
+    char *base = nullptr;
+    size_t used = 0, size = 0;
+    template <typename T>
+    T *take(size_t count)
+    {
+        size_t bytes = (count * sizeof(T) + 255) & ~size_t(255);
+        T *p = reinterpret_cast<T *>(base + used);
+        used += bytes;
+        return p;
+    }
+};
+
+struct TimedPair {
+    hipEvent_t a, b;
+    int kind;
+};
+
+}  // namespace
+
+struct mbots_handle {
+    mbots_config cfg{};
+    int device = 0;
+    mbots::SimState S{};
+    mbots::ObsTable T[2]{};
+    int tb = 0;
+    Arena arena;
+    int32_t *done_zeros = nullptr;    // Done column (never written, sim.cpp:74-75, B.7)
+    int32_t *reset_zeros = nullptr;   // WorldReset singleton per world
+    int32_t *sensor_index = nullptr;  // scratch for sensorIndexTensor
+    uint32_t *h_totals = nullptr;     // pinned mirror of S.totals
+    hipEvent_t ev_totals = nullptr;
+    hipStream_t last_stream = nullptr;
+    bool timing = false;
+    std::vector<TimedPair> pending;
+    std::vector<hipEvent_t> pool;
+    double acc_ms[MBOTS_TK_COUNT] = {};
+    uint64_t acc_n[MBOTS_TK_COUNT] = {};
+};
+
+namespace {
+
+hipEvent_t get_event(mbots_handle *h)
+{
+    if (!h->pool.empty()) {
+        hipEvent_t e = h->pool.back();
+        h->pool.pop_back();
+        return e;
+    }
+    hipEvent_t e = nullptr;
+    (void)hipEventCreate(&e);
+    return e;
+}
+
+template <typename F>
+int timed(mbots_handle *h, int kind, hipStream_t st, F &&launch)
+{
+    TimedPair tp{nullptr, nullptr, kind};
+    if (h->timing) {
+        tp.a = get_event(h);
+        tp.b = get_event(h);
+        HIP_TRY(hipEventRecord(tp.a, st));
+    }
+    HIP_TRY(launch());
+    if (h->timing) {
+        HIP_TRY(hipEventRecord(tp.b, st));
+        h->pending.push_back(tp);
+    }
+    return MBOTS_OK;
+}
+
+void fill_table(mbots::ObsTable &t, Arena &a, size_t rows)
+{
+    using namespace mbots;
+    t.species = a.take<int32_t>(rows);
+    t.pos = a.take<float>(rows * 2);
+    t.health = a.take<int32_t>(rows);
+    t.sur = a.take<float>(rows * 2);
+    t.reward = a.take<float>(rows);
+    t.action = a.take<int32_t>(rows * 6);
+    t.stats = a.take<int32_t>(rows * 4);
+    t.hidden = a.take<float>(rows * kHidden);
+    t.sem = a.take<int8_t>(rows * kSensor);
+    t.depth = a.take<uint8_t>(rows * kSensor);
+    t.pspecies = a.take<int32_t>(rows);
+    t.ppos = a.take<float>(rows * 2);
+    t.phealth = a.take<int32_t>(rows);
+    t.psur = a.take<float>(rows * 2);
+    t.preward = a.take<float>(rows);
+    t.paction = a.take<int32_t>(rows * 6);
+    t.pstats = a.take<int32_t>(rows * 4);
+    t.phidden = a.take<float>(rows * kHidden);
+    t.psem = a.take<int8_t>(rows * kSensor);
+    t.pdepth = a.take<uint8_t>(rows * kSensor);
+}
+
+size_t layout(mbots_handle *h, Arena &a)
+{
+    using namespace mbots;
+    const size_t W = h->cfg.num_worlds, cap = h->cfg.agent_capacity, rows = W * cap;
+    SimState &S = h->S;
+    S.x = a.take<float>(rows);
+    S.y = a.take<float>(rows);
+    S.rw = a.take<float>(rows);
+    S.rz = a.take<float>(rows);
+    S.species = a.take<int32_t>(rows);
+    S.health = a.take<int32_t>(rows);
+    S.finder = a.take<int32_t>(rows);
+    S.obsrow = a.take<int32_t>(rows);
+    S.sur0 = a.take<float>(rows);
+    S.sur1 = a.take<float>(rows);
+    S.stats = a.take<uint32_t>(rows);
+    S.n = a.take<int32_t>(W);
+    S.ctr = a.take<uint32_t>(W);
+    S.key = a.take<uint2>(W);
+    S.food = a.take<uint32_t>(W * kNumPkg);
+    S.cur_food = a.take<int32_t>(W);
+    S.sreward = a.take<float>(W * kNumSpecies);
+    S.scount = a.take<int32_t>(W * kNumSpecies);
+    S.row_base = a.take<int32_t>(W * kNumSpecies);
+    S.world_off = a.take<int32_t>(W);
+    S.overflow = a.take<uint32_t>(W);
+    S.totals = a.take<uint32_t>(8);
+    S.agent_steps = a.take<unsigned long long>(1);
+    fill_table(h->T[0], a, rows);
+    fill_table(h->T[1], a, rows);
+    h->done_zeros = a.take<int32_t>(rows);
+    h->reset_zeros = a.take<int32_t>(W);
+    h->sensor_index = a.take<int32_t>(rows);
+    return a.used;
+}
+
+hipStream_t as_stream(void *s) { return reinterpret_cast<hipStream_t>(s); }
+
+int sync_totals(mbots_handle *h)
+{
+    HIP_TRY(hipSetDevice(h->device));
+    HIP_TRY(hipEventSynchronize(h->ev_totals));
+    return MBOTS_OK;
+}
+
+int record_totals(mbots_handle *h, hipStream_t st)
+{
+    HIP_TRY(hipMemcpyAsync(h->h_totals, h->S.totals, 8 * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                           st));
+    HIP_TRY(hipEventRecord(h->ev_totals, st));
+    return MBOTS_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char *mbots_last_error(void) { return g_err.c_str(); }
+
+int mbots_create(const mbots_config *cfg_in, mbots_handle **out)
+{
+    if (!cfg_in || !out) return fail(MBOTS_E_INVALID, "null argument");
+    *out = nullptr;
+    mbots_config cfg = *cfg_in;
+    if (cfg.agent_capacity == 0) cfg.agent_capacity = 128;
+    if (cfg.sensor_size == 0) cfg.sensor_size = 32;
+    if (cfg.num_worlds == 0) return fail(MBOTS_E_INVALID, "num_worlds must be > 0");
+    if (cfg.sensor_size != (uint32_t)mbots::kSensor)
+        return fail(MBOTS_E_INVALID, "sensor_size must be 32 (mgr.hpp:19, entry.cpp:27)");
+    if (cfg.agent_capacity > (uint32_t)mbots::kMaxCap || cfg.agent_capacity < 4)
+        return fail(MBOTS_E_INVALID, "agent_capacity must be in [4, 128]");
+    if (cfg.init_num_agents_per_world > cfg.agent_capacity)
+        return fail(MBOTS_E_INVALID, "init_num_agents_per_world exceeds agent_capacity");
+    if (cfg.init_num_agents_per_world < (uint32_t)mbots::kNumSpecies)
+        return fail(MBOTS_E_INVALID, "init_num_agents_per_world must be >= 4");
+    const uint64_t rows = (uint64_t)cfg.num_worlds * cfg.agent_capacity;
+    if (rows >= (1ull << 31)) return fail(MBOTS_E_INVALID, "num_worlds * agent_capacity >= 2^31");
+
+    int ndev = 0;
+    HIP_TRY(hipGetDeviceCount(&ndev));
+    if (cfg.gpu_id < 0 || cfg.gpu_id >= ndev)
+        return fail(MBOTS_E_INVALID, "gpu_id out of range (" + std::to_string(ndev) + " devices)");
+    HIP_TRY(hipSetDevice(cfg.gpu_id));
+
+    mbots_handle *h = new mbots_handle();
+    h->cfg = cfg;
+    h->device = cfg.gpu_id;
+    Arena probe;
+    const size_t bytes = layout(h, probe);
+    if (hipMalloc(&h->arena.base, bytes) != hipSuccess) {
+        delete h;
+        return fail(MBOTS_E_NOMEM, "hipMalloc of " + std::to_string(bytes) + " bytes failed");
+    }
+    h->arena.size = bytes;
+    h->arena.used = 0;
+    layout(h, h->arena);
+    mbots::SimState &S = h->S;
+    S.W = cfg.num_worlds;
+    S.cap = cfg.agent_capacity;
+    S.A = cfg.init_num_agents_per_world;
+    S.world_offset = cfg.world_offset;
+    S.flags = cfg.flags;
+    S.seed = cfg.rand_seed;
+
+    int rc = MBOTS_OK;
+    auto check = [&](hipError_t e, const char *what) {
+        if (e != hipSuccess && rc == MBOTS_OK)
+            rc = fail(MBOTS_E_HIP, std::string(what) + ": " + hipGetErrorString(e));
+    };
+    check(hipHostMalloc((void **)&h->h_totals, 8 * sizeof(uint32_t), hipHostMallocDefault),
+          "hipHostMalloc");
+    check(hipEventCreateWithFlags(&h->ev_totals, hipEventDisableTiming), "hipEventCreate");
+    hipStream_t st = nullptr;
+    check(hipMemsetAsync(h->arena.base, 0, bytes, st), "hipMemsetAsync");
+    // Sim::Sim / initWorld (sim.cpp:1232-1256) + initial export of the rows
+    check(mbots::launch_init(S, st), "init_kernel");
+    check(mbots::launch_scan(S, st), "scan_kernel");
+    check(mbots::launch_export(S, h->T[1], h->T[0], 1, st), "export_kernel(init)");
+    if (rc == MBOTS_OK) rc = record_totals(h, st);
+    check(hipStreamSynchronize(st), "hipStreamSynchronize");
+    if (rc != MBOTS_OK) {
+        mbots_destroy(h);
+        return rc;
+    }
+    // the init scan counted the initial population as agent-steps; reset
+    unsigned long long zero = 0;
+    check(hipMemcpy(S.agent_steps, &zero, sizeof(zero), hipMemcpyHostToDevice), "hipMemcpy");
+    h->tb = 0;
+    *out = h;
+    return rc;
+}
+
+int mbots_destroy(mbots_handle *h)
+{
+    if (!h) return MBOTS_OK;
+    (void)hipSetDevice(h->device);
+    (void)hipDeviceSynchronize();
+    for (auto &p : h->pending) { (void)hipEventDestroy(p.a); (void)hipEventDestroy(p.b); }
+    for (auto e : h->pool) (void)hipEventDestroy(e);
+    if (h->ev_totals) (void)hipEventDestroy(h->ev_totals);
+    if (h->h_totals) (void)hipHostFree(h->h_totals);
+    if (h->arena.base) (void)hipFree(h->arena.base);
+    delete h;
+    return MBOTS_OK;
+}
+
+int mbots_step(mbots_handle *h, void *stream)
+{
+    if (!h) return fail(MBOTS_E_INVALID, "null handle");
+    HIP_TRY(hipSetDevice(h->device));
+    hipStream_t st = as_stream(stream);
+    h->last_stream = st;
+    const mbots::ObsTable &cur = h->T[h->tb];
+    const mbots::ObsTable &nxt = h->T[h->tb ^ 1];
+    int rc;
+    if ((rc = timed(h, MBOTS_TK_WORLD_STEP, st, [&] { return mbots::launch_world_step(h->S, cur, st); })))
+        return rc;
+    if ((rc = timed(h, MBOTS_TK_SCAN, st, [&] { return mbots::launch_scan(h->S, st); }))) return rc;
+    if ((rc = timed(h, MBOTS_TK_EXPORT, st, [&] { return mbots::launch_export(h->S, cur, nxt, 0, st); })))
+        return rc;
+    if ((rc = timed(h, MBOTS_TK_SENSOR, st, [&] { return mbots::launch_sensor(h->S, nxt, st); })))
+        return rc;
+    h->tb ^= 1;
+    return record_totals(h, st);
+}
+
+int mbots_shift_observations(mbots_handle *h, void *stream)
+{
+    if (!h) return fail(MBOTS_E_INVALID, "null handle");
+    HIP_TRY(hipSetDevice(h->device));
+    hipStream_t st = as_stream(stream);
+    h->last_stream = st;
+    return timed(h, MBOTS_TK_SHIFT, st, [&] { return mbots::launch_shift(h->S, h->T[h->tb], st); });
+}
+
+int mbots_num_agents(mbots_handle *h, uint32_t *out)
+{
+    if (!h || !out) return fail(MBOTS_E_INVALID, "null argument");
+    int rc = sync_totals(h);
+    if (rc) return rc;
+    *out = h->h_totals[0];
+    return MBOTS_OK;
+}
+
+int mbots_export(mbots_handle *h, int32_t id, mbots_tensor *out)
+{
+    using namespace mbots;
+    if (!h || !out) return fail(MBOTS_E_INVALID, "null argument");
+    uint32_t N = 0;
+    int rc = mbots_num_agents(h, &N);
+    if (rc) return rc;
+    const ObsTable &t = h->T[h->tb];
+    const bool fixd = (h->cfg.flags & MBOTS_FLAG_FIX_DEPTH_ALIAS) != 0;
+    void *p = nullptr;
+    int dt = MBOTS_DTYPE_INT32;
+    int64_t rows = N, cols = 1;
+    switch (id) {
+    case MBOTS_EXPORT_RESET: p = h->reset_zeros; rows = h->cfg.num_worlds; break;
+    case MBOTS_EXPORT_ACTION: p = t.action; cols = 6; break;
+    case MBOTS_EXPORT_PREV_ACTION: p = t.paction; cols = 6; break;
+    case MBOTS_EXPORT_HIDDEN_STATE: p = t.hidden; dt = MBOTS_DTYPE_FLOAT32; cols = kHidden; break;
+    case MBOTS_EXPORT_PREV_HIDDEN_STATE: p = t.phidden; dt = MBOTS_DTYPE_FLOAT32; cols = kHidden; break;
+    case MBOTS_EXPORT_REWARD: p = t.reward; dt = MBOTS_DTYPE_FLOAT32; break;
+    case MBOTS_EXPORT_PREV_REWARD: p = t.preward; dt = MBOTS_DTYPE_FLOAT32; break;
+    case MBOTS_EXPORT_DONE: p = h->done_zeros; break;
+    case MBOTS_EXPORT_POSITION: p = t.pos; dt = MBOTS_DTYPE_FLOAT32; cols = 2; break;
+    case MBOTS_EXPORT_PREV_POSITION: p = t.ppos; dt = MBOTS_DTYPE_FLOAT32; cols = 2; break;
+    // int32 health bits exported as a float32 view (types.hpp:119-124, mgr.cpp:397-414; B.2)
+    case MBOTS_EXPORT_HEALTH: p = t.health; dt = MBOTS_DTYPE_FLOAT32; break;
+    case MBOTS_EXPORT_PREV_HEALTH: p = t.phealth; dt = MBOTS_DTYPE_FLOAT32; break;
+    case MBOTS_EXPORT_SURROUNDING: p = t.sur; dt = MBOTS_DTYPE_FLOAT32; cols = 2; break;
+    case MBOTS_EXPORT_PREV_SURROUNDING: p = t.psur; dt = MBOTS_DTYPE_FLOAT32; cols = 2; break;
+    case MBOTS_EXPORT_SENSOR_SEMANTIC: p = t.sem; dt = MBOTS_DTYPE_INT8; cols = kSensor; break;
+    // SensorDepth exports the semantic buffer (sim.cpp:102-104, B.1) unless fixed
+    case MBOTS_EXPORT_SENSOR_DEPTH:
+        p = fixd ? (void *)t.depth : (void *)t.sem; dt = MBOTS_DTYPE_UINT8; cols = kSensor; break;
+    case MBOTS_EXPORT_PREV_SENSOR_SEMANTIC: p = t.psem; dt = MBOTS_DTYPE_INT8; cols = kSensor; break;
+    case MBOTS_EXPORT_PREV_SENSOR_DEPTH:
+        p = fixd ? (void *)t.pdepth : (void *)t.psem; dt = MBOTS_DTYPE_UINT8; cols = kSensor; break;
+    case MBOTS_EXPORT_STATS: p = t.stats; cols = 4; break;
+    case MBOTS_EXPORT_PREV_STATS: p = t.pstats; cols = 4; break;
+    case MBOTS_EXPORT_SENSOR_INDEX: {
+        hipStream_t st = h->last_stream;
+        HIP_TRY(mbots::launch_sensor_index(h->S, h->sensor_index, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        p = h->sensor_index;
+        break;
+    }
+    case MBOTS_EXPORT_SPECIES_COUNT: p = h->S.scount; rows = h->cfg.num_worlds; cols = kNumSpecies; break;
+    case MBOTS_EXPORT_SPECIES: p = t.species; break;
+    case MBOTS_EXPORT_PREV_SPECIES: p = t.pspecies; break;
+    default: return fail(MBOTS_E_INVALID, "unknown export id " + std::to_string(id));
+    }
+    out->data = p;
+    out->dtype = dt;
+    out->device = h->device;
+    out->dims[0] = rows;
+    out->dims[1] = cols;
+    return MBOTS_OK;
+}
+
+int mbots_set_action(mbots_handle *h, uint32_t row, const int32_t action[6])
+{
+    if (!h || !action) return fail(MBOTS_E_INVALID, "null argument");
+    uint32_t N = 0;
+    int rc = mbots_num_agents(h, &N);
+    if (rc) return rc;
+    if (row >= N) return fail(MBOTS_E_RANGE, "agent row out of range");
+    HIP_TRY(hipMemcpy(h->T[h->tb].action + (size_t)row * 6, action, 6 * sizeof(int32_t),
+                      hipMemcpyHostToDevice));
+    return MBOTS_OK;
+}
+
+int mbots_agent_offset_for_world(mbots_handle *h, uint32_t world, uint32_t *out)
+{
+    if (!h || !out) return fail(MBOTS_E_INVALID, "null argument");
+    if (world >= h->cfg.num_worlds) return fail(MBOTS_E_RANGE, "world out of range");
+    int rc = sync_totals(h);
+    if (rc) return rc;
+    int32_t v = 0;
+    HIP_TRY(hipMemcpy(&v, h->S.world_off + world, sizeof(v), hipMemcpyDeviceToHost));
+    *out = (uint32_t)v;
+    return MBOTS_OK;
+}
+
+int mbots_write_synthetic_actions(mbots_handle *h, uint32_t seed, uint32_t step,
+                                  int32_t write_hidden, void *stream)
+{
+    if (!h) return fail(MBOTS_E_INVALID, "null handle");
+    HIP_TRY(hipSetDevice(h->device));
+    hipStream_t st = as_stream(stream);
+    return timed(h, MBOTS_TK_ACTIONS, st, [&] {
+        return mbots::launch_synthetic_actions(h->S, h->T[h->tb], seed, step, write_hidden, st);
+    });
+}
+
+int mbots_agent_steps(mbots_handle *h, uint64_t *out)
+{
+    if (!h || !out) return fail(MBOTS_E_INVALID, "null argument");
+    HIP_TRY(hipSetDevice(h->device));
+    HIP_TRY(hipDeviceSynchronize());
+    unsigned long long v = 0;
+    HIP_TRY(hipMemcpy(&v, h->S.agent_steps, sizeof(v), hipMemcpyDeviceToHost));
+    *out = v;
+    return MBOTS_OK;
+}
+
+int mbots_overflow(mbots_handle *h, uint64_t *out)
+{
+    if (!h || !out) return fail(MBOTS_E_INVALID, "null argument");
+    HIP_TRY(hipSetDevice(h->device));
+    HIP_TRY(hipDeviceSynchronize());
+    std::vector<uint32_t> v(h->cfg.num_worlds);
+    HIP_TRY(hipMemcpy(v.data(), h->S.overflow, v.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    uint64_t s = 0;
+    for (uint32_t x : v) s += x;
+    *out = s;
+    return MBOTS_OK;
+}
+
+int mbots_enable_kernel_timing(mbots_handle *h, int32_t enable)
+{
+    if (!h) return fail(MBOTS_E_INVALID, "null handle");
+    HIP_TRY(hipSetDevice(h->device));
+    HIP_TRY(hipDeviceSynchronize());
+    for (auto &p : h->pending) { h->pool.push_back(p.a); h->pool.push_back(p.b); }
+    h->pending.clear();
+    for (int k = 0; k < MBOTS_TK_COUNT; ++k) { h->acc_ms[k] = 0.0; h->acc_n[k] = 0; }
+    h->timing = enable != 0;
+    return MBOTS_OK;
+}
+
+int mbots_kernel_times(mbots_handle *h, double ms[MBOTS_TK_COUNT], uint64_t launches[MBOTS_TK_COUNT])
+{
+    if (!h) return fail(MBOTS_E_INVALID, "null handle");
+    HIP_TRY(hipSetDevice(h->device));
+    for (auto &p : h->pending) {
+        HIP_TRY(hipEventSynchronize(p.b));
+        float t = 0.0f;
+        HIP_TRY(hipEventElapsedTime(&t, p.a, p.b));
+        h->acc_ms[p.kind] += t;
+        h->acc_n[p.kind] += 1;
+        h->pool.push_back(p.a);
+        h->pool.push_back(p.b);
+    }
+    h->pending.clear();
+    for (int k = 0; k < MBOTS_TK_COUNT; ++k) {
+        if (ms) ms[k] = h->acc_ms[k];
+        if (launches) launches[k] = h->acc_n[k];
+    }
+    return MBOTS_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,262 @@
+"""madrona_bots -- MI355X-native drop-in for the reference's Python module.
+
+Mirrors the nanobind surface of src/entry/entry.cpp:16-45:
+
+    SimManager(gpu_id, num_worlds, rand_seed, init_num_agents_per_world)
+        .step()  .shift_observations()
+        .depth_tensor(is_prev)  .semantic_tensor(is_prev)  .reward_tensor(is_prev)
+        .species_count_tensor() .position_tensor(is_prev)  .health_tensor(is_prev)
+        .surrounding_tensor(is_prev)  .action_tensor(is_prev)
+        .stats_tensor(is_prev)  .hidden_state_tensor(is_prev)
+
+Each accessor returns a ``Tensor`` whose ``to_torch()`` is a zero-copy torch
+view of device memory owned by the manager (madrona::py::Tensor,
+mgr.cpp:138-144).  The simulation runs in libmbots.so (hand-written gfx950
+kernels); there is no CPU fallback -- importing without the built library
+raises ImportError.
+"""
+import ctypes
+import os
+import types
+
+import torch  # loads the HIP runtime libmbots.so links against (same soname)
+
+__all__ = ["SimManager", "Tensor", "madrona", "ExportID"]
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "libmbots.so")
+
+if not os.path.exists(_LIB_PATH):
+    raise ImportError(
+        f"madrona_bots: {_LIB_PATH} is missing; build it with "
+        "`python -c 'import __graft_entry__ as g; g.build()'` (hipcc, gfx950)")
+
+
+class _Config(ctypes.Structure):
+    _fields_ = [("gpu_id", ctypes.c_int32), ("num_worlds", ctypes.c_uint32),
+                ("rand_seed", ctypes.c_uint32), ("init_num_agents_per_world", ctypes.c_uint32),
+                ("sensor_size", ctypes.c_uint32), ("world_offset", ctypes.c_uint32),
+                ("agent_capacity", ctypes.c_uint32), ("flags", ctypes.c_uint32)]
+
+
+class _CTensor(ctypes.Structure):
+    _fields_ = [("data", ctypes.c_void_p), ("dtype", ctypes.c_int32), ("device", ctypes.c_int32),
+                ("dims", ctypes.c_int64 * 2)]
+
+
+def _load():
+    L = ctypes.CDLL(_LIB_PATH)
+    vp, i32, u32 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_uint32
+    P = ctypes.POINTER
+    sig = {
+        "mbots_create": [P(_Config), P(vp)],
+        "mbots_destroy": [vp],
+        "mbots_step": [vp, vp],
+        "mbots_shift_observations": [vp, vp],
+        "mbots_num_agents": [vp, P(u32)],
+        "mbots_export": [vp, i32, P(_CTensor)],
+        "mbots_set_action": [vp, u32, P(i32)],
+        "mbots_agent_offset_for_world": [vp, u32, P(u32)],
+        "mbots_write_synthetic_actions": [vp, u32, u32, i32, vp],
+        "mbots_agent_steps": [vp, P(ctypes.c_uint64)],
+        "mbots_overflow": [vp, P(ctypes.c_uint64)],
+        "mbots_enable_kernel_timing": [vp, i32],
+        "mbots_kernel_times": [vp, P(ctypes.c_double), P(ctypes.c_uint64)],
+    }
+    for name, args in sig.items():
+        fn = getattr(L, name)
+        fn.argtypes = args
+        fn.restype = ctypes.c_int
+    L.mbots_last_error.restype = ctypes.c_char_p
+    L.mbots_last_error.argtypes = []
+    return L
+
+
+_lib = _load()
+
+
+def _check(rc):
+    if rc != 0:
+        msg = _lib.mbots_last_error().decode(errors="replace")
+        raise RuntimeError(f"madrona_bots: {msg} (status {rc})")
+
+
+class ExportID:
+    """enum class ExportID (src/sim/sim.hpp:18-55) + build extensions."""
+    Reset, Action, PrevAction, HiddenState, PrevHiddenState, Reward, PrevReward, Done, \
+        Position, PrevPosition, Health, PrevHealth, Surrounding, PrevSurrounding, \
+        SensorSemantic, SensorDepth, PrevSensorSemantic, PrevSensorDepth, Stats, PrevStats, \
+        SensorIndex, SpeciesCount = range(22)
+    Species, PrevSpecies = 32, 33
+
+
+_DTYPES = {0: (torch.uint8, "|u1"), 1: (torch.int8, "|i1"), 2: (torch.int32, "<i4"),
+           3: (torch.float32, "<f4")}
+
+FLAG_REWARD_FIXED = 0x1
+FLAG_FIX_DEPTH_ALIAS = 0x2
+
+# TK_* indices of mbots_kernel_times
+KERNELS = ("world_step", "scan", "export", "sensor", "shift", "actions")
+
+
+class Tensor:
+    """Non-owning device tensor view (madrona::py::Tensor)."""
+
+    def __init__(self, owner, ct):
+        self._owner = owner          # keeps the manager (and its memory) alive
+        self._ptr = int(ct.data or 0)
+        self._torch_dtype, self._typestr = _DTYPES[ct.dtype]
+        self._device = int(ct.device)
+        self.shape = (int(ct.dims[0]), int(ct.dims[1]))
+
+    def devicePtr(self):
+        return self._ptr
+
+    @property
+    def dtype(self):
+        return self._torch_dtype
+
+    @property
+    def __cuda_array_interface__(self):
+        return {"shape": self.shape, "typestr": self._typestr, "data": (self._ptr, False),
+                "version": 3, "strides": None, "stream": None}
+
+    def to_torch(self):
+        """Zero-copy torch view on cuda:<gpu_id>."""
+        dev = torch.device("cuda", self._device)
+        if self.shape[0] == 0:
+            return torch.empty(self.shape, dtype=self._torch_dtype, device=dev)
+        t = torch.as_tensor(self, device=dev)
+        if t.data_ptr() != self._ptr:
+            raise RuntimeError("madrona_bots: to_torch() produced a copy, expected a view")
+        return t
+
+
+madrona = types.ModuleType("madrona_bots.madrona")
+madrona.Tensor = Tensor
+
+
+class SimManager:
+    """Manager (src/entry/mgr.hpp:10-68) with the nanobind constructor
+    signature (entry.cpp:17-28).  Keyword-only extensions: agent_capacity
+    (per-world slot cap), world_offset (global index of this shard's first
+    world), reward_fixed (rewards[speciesID-1] instead of the reference's
+    off-by-one), fix_depth_alias (depth_tensor returns real depth,
+    SURVEY B.1)."""
+
+    def __init__(self, gpu_id, num_worlds, rand_seed, init_num_agents_per_world, *,
+                 agent_capacity=128, world_offset=0, reward_fixed=False,
+                 fix_depth_alias=False):
+        self.gpu_id = int(gpu_id)
+        self.num_worlds = int(num_worlds)
+        flags = (FLAG_REWARD_FIXED if reward_fixed else 0) | \
+                (FLAG_FIX_DEPTH_ALIAS if fix_depth_alias else 0)
+        cfg = _Config(self.gpu_id, self.num_worlds, int(rand_seed) & 0xFFFFFFFF,
+                      int(init_num_agents_per_world), 32, int(world_offset),
+                      int(agent_capacity), flags)
+        h = ctypes.c_void_p()
+        _check(_lib.mbots_create(ctypes.byref(cfg), ctypes.byref(h)))
+        self._h = h
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h:
+            _lib.mbots_destroy(h)
+            self._h = None
+
+    def _stream(self):
+        return ctypes.c_void_p(torch.cuda.current_stream(self.gpu_id).cuda_stream)
+
+    # -- graphs -------------------------------------------------------------
+    def step(self):
+        _check(_lib.mbots_step(self._h, self._stream()))
+
+    def shift_observations(self):
+        _check(_lib.mbots_shift_observations(self._h, self._stream()))
+
+    # -- exports ------------------------------------------------------------
+    def _export(self, eid):
+        ct = _CTensor()
+        _check(_lib.mbots_export(self._h, eid, ctypes.byref(ct)))
+        return Tensor(self, ct)
+
+    def depth_tensor(self, is_prev=False):
+        return self._export(ExportID.PrevSensorDepth if is_prev else ExportID.SensorDepth)
+
+    def semantic_tensor(self, is_prev=False):
+        return self._export(ExportID.PrevSensorSemantic if is_prev else ExportID.SensorSemantic)
+
+    def reward_tensor(self, is_prev=False):
+        return self._export(ExportID.PrevReward if is_prev else ExportID.Reward)
+
+    def species_count_tensor(self):
+        return self._export(ExportID.SpeciesCount)
+
+    def position_tensor(self, is_prev=False):
+        return self._export(ExportID.PrevPosition if is_prev else ExportID.Position)
+
+    def health_tensor(self, is_prev=False):
+        return self._export(ExportID.PrevHealth if is_prev else ExportID.Health)
+
+    def surrounding_tensor(self, is_prev=False):
+        return self._export(ExportID.PrevSurrounding if is_prev else ExportID.Surrounding)
+
+    def action_tensor(self, is_prev=False):
+        return self._export(ExportID.PrevAction if is_prev else ExportID.Action)
+
+    def stats_tensor(self, is_prev=False):
+        return self._export(ExportID.PrevStats if is_prev else ExportID.Stats)
+
+    def hidden_state_tensor(self, is_prev=False):
+        return self._export(ExportID.PrevHiddenState if is_prev else ExportID.HiddenState)
+
+    # C++-only accessors of the reference (mgr.hpp:38, :54-62) + extensions
+    def sensor_index_tensor(self):
+        return self._export(ExportID.SensorIndex)
+
+    def done_tensor(self):
+        return self._export(ExportID.Done)
+
+    def species_tensor(self, is_prev=False):
+        return self._export(ExportID.PrevSpecies if is_prev else ExportID.Species)
+
+    def set_action(self, agent_idx, forward, backward, rotate_left, rotate_right, shoot, breed):
+        a = (ctypes.c_int32 * 6)(forward, backward, rotate_left, rotate_right, shoot, breed)
+        _check(_lib.mbots_set_action(self._h, int(agent_idx), a))
+
+    def agent_offset_for_world(self, world_idx):
+        v = ctypes.c_uint32()
+        _check(_lib.mbots_agent_offset_for_world(self._h, int(world_idx), ctypes.byref(v)))
+        return v.value
+
+    # -- build utilities ------------------------------------------------------
+    def num_agents(self):
+        v = ctypes.c_uint32()
+        _check(_lib.mbots_num_agents(self._h, ctypes.byref(v)))
+        return v.value
+
+    def write_synthetic_actions(self, seed, step, write_hidden=False):
+        _check(_lib.mbots_write_synthetic_actions(self._h, int(seed) & 0xFFFFFFFF,
+                                                  int(step) & 0xFFFFFFFF,
+                                                  1 if write_hidden else 0, self._stream()))
+
+    def agent_steps(self):
+        v = ctypes.c_uint64()
+        _check(_lib.mbots_agent_steps(self._h, ctypes.byref(v)))
+        return v.value
+
+    def overflow(self):
+        v = ctypes.c_uint64()
+        _check(_lib.mbots_overflow(self._h, ctypes.byref(v)))
+        return v.value
+
+    def enable_kernel_timing(self, enable=True):
+        _check(_lib.mbots_enable_kernel_timing(self._h, 1 if enable else 0))
+
+    def kernel_times(self):
+        """{kernel: (total_ms, launches)} since enable_kernel_timing()."""
+        ms = (ctypes.c_double * len(KERNELS))()
+        n = (ctypes.c_uint64 * len(KERNELS))()
+        _check(_lib.mbots_kernel_times(self._h, ms, n))
+        return {k: (ms[i], n[i]) for i, k in enumerate(KERNELS)}
