@@ -514,15 +514,25 @@ __global__ __launch_bounds__(256) void export_kernel(SimState S, ObsTable cur, O
 // ---------------------------------------------------------------------------
 // K4: sensor -- 32-pixel raycast (24 forward + 8 backward) plus the finder ray
 // (Madrona RenderingSystem, sim.cpp:1183-1188; spec DESIGN.md 3.6).
-// One wave per world; lanes sweep (agent, ray) pairs; objects staged in LDS.
+// One wave per world.  Pass A culls every (agent, object) pair to the pixels
+// whose ray can reach the object's inflated bounding circle and records them
+// in per-(agent, pixel) candidate bitmasks in LDS; pass B casts each pixel's
+// ray exactly against the 4 walls and its candidates only, in the fixed object
+// order (food, then agents by slot) with strict '<' -- the same result as
+// testing every object.  Culling uses approximate math with margins; the exact
+// tests decide every hit.
 // ---------------------------------------------------------------------------
+constexpr int kMaskWords = 1152;              // 4.5 KiB of candidate masks per world
+constexpr int kMaxFood = kFoodCap + 2;        // live packages == currentNumFood <= 30
+constexpr float kRCircle = 1.0f + 0.05f;      // cull radius of a unit circle
+constexpr float kRBox = 1.41421356f + 0.05f;  // cull radius of a unit half-extent box
+constexpr float kNearPad = 0.5f;              // |f| <= R + pad: every pixel
+
 struct SensorLDS {
-    float ax[kMaxCap], ay[kMaxCap], dx[kMaxCap], dy[kMaxCap];
+    float ox[kMaxFood + kMaxCap], oy[kMaxFood + kMaxCap];   // food then agents
+    float hx[kMaxCap], hy[kMaxCap];
     int32_t sp[kMaxCap];
-    float fx[kNumPkg], fy[kNumPkg];
-    int8_t sem[kMaxCap * kSensor];
-    uint8_t dep[kMaxCap * kSensor];
-    int32_t nfood;
+    uint32_t mask[kMaskWords];
 };
 
 __constant__ float kWallBox[4][4] = {
@@ -531,6 +541,53 @@ __constant__ float kWallBox[4][4] = {
     {64.0f - 64.0f, 64.0f + 64.0f, 96.0f - 0.2f, 96.0f + 0.2f},
     {128.0f - 0.2f, 128.0f + 0.2f, 48.0f - 48.0f, 48.0f + 48.0f},
 };
+
+__device__ __forceinline__ int clamp_floor(float v, int lo, int hi)
+{
+    v = fminf(fmaxf(v, (float)lo - 1.0f), (float)hi + 1.0f);
+    return (int)floorf(v);
+}
+__device__ __forceinline__ int clamp_ceil(float v, int lo, int hi)
+{
+    v = fminf(fmaxf(v, (float)lo - 1.0f), (float)hi + 1.0f);
+    return (int)ceilf(v);
+}
+
+// exact cast of one ray against walls + candidate bitmask (object order)
+__device__ __forceinline__ int cast_candidates(const SensorLDS &L, const Ray &ray,
+                                               const uint32_t *mk, int words, int nf,
+                                               float &best, int &slot)
+{
+    best = __builtin_inff();
+    int sem = -1;
+    slot = -1;
+    float t;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        if (ray_box(ray, kWallBox[k][0], kWallBox[k][1], kWallBox[k][2], kWallBox[k][3], t) &&
+            t < best) {
+            best = t; sem = 5; slot = -1;
+        }
+    }
+    for (int wd = 0; wd < words; ++wd) {
+        uint32_t m = mk[wd];
+        while (m) {
+            const int j = wd * 32 + __builtin_ctz(m);
+            m &= m - 1u;
+            const float cx = L.ox[j], cy = L.oy[j];
+            if (j < nf) {
+                if (ray_box(ray, cx - 1.0f, cx + 1.0f, cy - 1.0f, cy + 1.0f, t) && t < best) {
+                    best = t; sem = 6; slot = -1;
+                }
+            } else {
+                if (ray_circle(ray, cx, cy, t) && t < best) {
+                    best = t; sem = L.sp[j - nf]; slot = j - nf;
+                }
+            }
+        }
+    }
+    return sem;
+}
 
 __global__ __launch_bounds__(256) void sensor_kernel(SimState S, ObsTable nxt)
 {
@@ -543,20 +600,12 @@ __global__ __launch_bounds__(256) void sensor_kernel(SimState S, ObsTable nxt)
     const size_t base = (size_t)w * S.cap;
     const int n = S.n[w];
     const bool depth = (S.flags & kFlagFixDepth) != 0;
-    for (int i = lane; i < n; i += 64) {
-        L.ax[i] = S.x[base + i];
-        L.ay[i] = S.y[base + i];
-        L.sp[i] = S.species[base + i];
-        float dx, dy;
-        heading(S.rw[base + i], S.rz[base + i], dx, dy);
-        L.dx[i] = dx;
-        L.dy[i] = dy;
-    }
-    // live food packages in (chunk, package) order
+
+    // live food packages in (chunk, package) order -> objects [0, nf)
     int nf = 0;
     for (int b = 0; b < kNumPkg; b += 64) {
         const int k = b + (int)lane;
-        uint32_t p = k < kNumPkg ? S.food[(size_t)w * kNumPkg + k] : 0u;
+        const uint32_t p = k < kNumPkg ? S.food[(size_t)w * kNumPkg + k] : 0u;
         const bool live = (p >> 16) != 0u;
         const uint64_t m = ballot64(live);
         if (live) {
@@ -564,69 +613,142 @@ __global__ __launch_bounds__(256) void sensor_kernel(SimState S, ObsTable nxt)
             const float bx = (float)((c % kChunksX) * kChunkW);
             const float by = (float)((c / kChunksX) * kChunkW);
             const int s = nf + (int)rank_below(m);
-            L.fx[s] = (float)(p & 0xFFu) + bx;
-            L.fy[s] = (float)((p >> 8) & 0xFFu) + by;
+            if (s < kMaxFood) {   // live packages == currentNumFood <= 30 (addFoodSystem)
+                L.ox[s] = (float)(p & 0xFFu) + bx;
+                L.oy[s] = (float)((p >> 8) & 0xFFu) + by;
+            }
         }
         nf += __popcll(m);
     }
-    wave_sync();
-    const int npairs = n * kRays;
-    for (int p = lane; p < npairs; p += 64) {
-        const int i = p / kRays, ray = p - i * kRays;
-        const float ox = L.ax[i], oy = L.ay[i], hx = L.dx[i], hy = L.dy[i];
-        const float rx = hy, ry = -hx;
+    nf = min(nf, kMaxFood);
+    // agents -> objects [nf, nf + n)
+    for (int i = lane; i < n; i += 64) {
+        L.ox[nf + i] = S.x[base + i];
+        L.oy[nf + i] = S.y[base + i];
+        L.sp[i] = S.species[base + i];
         float dx, dy;
-        if (ray < 24) {
-            const float u = (float)(2 * ray + 1) / 24.0f - 1.0f;
-            dx = hx + u * rx;
-            dy = hy + u * ry;
-        } else if (ray < kSensor) {
-            const float u = (float)(2 * (ray - 24) + 1) / 8.0f - 1.0f;
-            dx = -(hx + u * rx);
-            dy = -(hy + u * ry);
-        } else {
-            dx = hx;
-            dy = hy;
-        }
-        float best = __builtin_inff(), t;
-        int sem = -1, slot = -1;
-        for (int k = 0; k < 4; ++k) {
-            if (ray_box(ox, oy, dx, dy, kWallBox[k][0], kWallBox[k][1], kWallBox[k][2],
-                        kWallBox[k][3], t) && t < best) {
-                best = t; sem = 5; slot = -1;
+        heading(S.rw[base + i], S.rz[base + i], dx, dy);
+        L.hx[i] = dx;
+        L.hy[i] = dy;
+    }
+    const int nobj = nf + n;
+    const int words = (nobj + 31) >> 5;
+    const int per_agent = kRays * words;
+    const int chunk = max(1, min(n, kMaskWords / per_agent));
+    wave_sync();
+
+    for (int a0 = 0; a0 < n; a0 += chunk) {
+        const int nc = min(chunk, n - a0);
+        for (int q = lane; q < nc * per_agent; q += 64) L.mask[q] = 0u;
+        wave_sync();
+        // ---- pass A: (agent, object) -> candidate pixels ----
+        for (int ii = 0; ii < nc; ++ii) {
+            const int i = a0 + ii;
+            const float ax = L.ox[nf + i], ay = L.oy[nf + i], hx = L.hx[i], hy = L.hy[i];
+            uint32_t *mk = L.mask + ii * per_agent;
+            for (int j = lane; j < nobj; j += 64) {
+                if (j == nf + i) continue;   // no self hits
+                const float R = j < nf ? kRBox : kRCircle;
+                const float vx = L.ox[j] - ax, vy = L.oy[j] - ay;
+                const float f = vx * hx + vy * hy;   // along the heading
+                const float l = vx * hy - vy * hx;   // along r = (hy, -hx)
+                int plo = 0, phi = 23, blo = 0, bhi = 7;
+                bool fwd, bwd, fnd;
+                const float af = fabsf(f), al = fabsf(l);
+                if (af > R + kNearPad) {
+                    // bounding circle wholly in front / behind: pixel interval from
+                    // (l - u f)^2 <= R^2 (1 + u^2)  (ray direction d + u r)
+                    const float A = f * f - R * R;
+                    const float s = __builtin_amdgcn_sqrtf(f * f + l * l - R * R);
+                    const float ia = __builtin_amdgcn_rcpf(A);
+                    const float u1 = (l * f - R * s) * ia, u2 = (l * f + R * s) * ia;
+                    if (f > 0.0f) {
+                        bwd = false;
+                        plo = clamp_ceil((u1 + 1.0f) * 12.0f - 0.5f - 0.02f, 0, 23);
+                        phi = clamp_floor((u2 + 1.0f) * 12.0f - 0.5f + 0.02f, 0, 23);
+                        fwd = plo <= phi;
+                        fnd = (u1 - 1e-3f <= 0.0f) && (u2 + 1e-3f >= 0.0f);
+                    } else {
+                        fwd = false;
+                        fnd = false;
+                        blo = clamp_ceil((u1 + 1.0f) * 4.0f - 0.5f - 0.02f, 0, 7);
+                        bhi = clamp_floor((u2 + 1.0f) * 4.0f - 0.5f + 0.02f, 0, 7);
+                        bwd = blo <= bhi;
+                    }
+                } else {
+                    // beside the agent: test against the 90-degree view wedges
+                    // |l| <= f (forward) and |l| <= -f (backward); every pixel of a
+                    // wedge the circle may touch
+                    const float lim = R * 1.41421356f + 0.05f;
+                    fwd = (al - f <= lim) && (f >= -R - 0.05f);
+                    bwd = (al + f <= lim) && (f <= R + 0.05f);
+                    fnd = (al <= R + 0.05f) && (f >= -R - 0.05f);
+                }
+                const uint32_t bit = 1u << (j & 31);
+                const int wd = j >> 5;
+                if (fwd) {
+                    for (int p = max(plo, 0); p <= min(phi, 23); ++p) atomicOr(&mk[p * words + wd], bit);
+                }
+                if (bwd) {
+                    for (int p = max(blo, 0); p <= min(bhi, 7); ++p)
+                        atomicOr(&mk[(24 + p) * words + wd], bit);
+                }
+                if (fnd) atomicOr(&mk[kSensor * words + wd], bit);
             }
         }
-        for (int f = 0; f < nf; ++f) {
-            const float fx = L.fx[f], fy = L.fy[f];
-            if (ray_box(ox, oy, dx, dy, fx - 1.0f, fx + 1.0f, fy - 1.0f, fy + 1.0f, t) &&
-                t < best) {
-                best = t; sem = 6; slot = -1;
+        wave_sync();
+        // ---- pass B: 32 pixel rays, two agents per wave ----
+        for (int pb = 0; pb < nc; pb += 2) {
+            const int ii = pb + (int)(lane >> 5);
+            const int px = (int)(lane & 31u);
+            const bool valid = ii < nc;
+            uint32_t semv = 0u, depv = 0u;
+            if (valid) {
+                const int i = a0 + ii;
+                const float hx = L.hx[i], hy = L.hy[i];
+                const float rx = hy, ry = -hx;
+                float dx, dy;
+                if (px < 24) {
+                    const float u = (float)(2 * px + 1) / 24.0f - 1.0f;
+                    dx = hx + u * rx;
+                    dy = hy + u * ry;
+                } else {
+                    const float u = (float)(2 * (px - 24) + 1) / 8.0f - 1.0f;
+                    dx = -(hx + u * rx);
+                    dy = -(hy + u * ry);
+                }
+                const Ray ray = make_ray(L.ox[nf + i], L.oy[nf + i], dx, dy);
+                float best;
+                int slot;
+                const int sem = cast_candidates(L, ray, L.mask + ii * per_agent + px * words, words,
+                                                nf, best, slot);
+                semv = (uint32_t)(uint8_t)(int8_t)sem;
+                depv = depth_u8(best);
+            }
+            // pack 4 lanes' bytes into one dword and store 32-B rows
+            semv <<= 8u * (lane & 3u);
+            depv <<= 8u * (lane & 3u);
+            semv |= __shfl_xor(semv, 1);
+            semv |= __shfl_xor(semv, 2);
+            depv |= __shfl_xor(depv, 1);
+            depv |= __shfl_xor(depv, 2);
+            if (valid && (lane & 3u) == 0u) {
+                const size_t r = (size_t)S.obsrow[base + a0 + ii];
+                reinterpret_cast<uint32_t *>(nxt.sem + r * kSensor)[px >> 2] = semv;
+                if (depth) reinterpret_cast<uint32_t *>(nxt.depth + r * kSensor)[px >> 2] = depv;
             }
         }
-        for (int j = 0; j < n; ++j) {
-            if (j == i) continue;
-            if (ray_circle(ox, oy, dx, dy, L.ax[j], L.ay[j], t) && t < best) {
-                best = t; sem = L.sp[j]; slot = j;
-            }
-        }
-        if (ray < kSensor) {
-            L.sem[i * kSensor + ray] = (int8_t)sem;
-            if (depth) L.dep[i * kSensor + ray] = depth_u8(best);
-        } else {
+        // ---- finder ray (forward centre) ----
+        for (int ii = lane; ii < nc; ii += 64) {
+            const int i = a0 + ii;
+            const Ray ray = make_ray(L.ox[nf + i], L.oy[nf + i], L.hx[i], L.hy[i]);
+            float best;
+            int slot;
+            (void)cast_candidates(L, ray, L.mask + ii * per_agent + kSensor * words, words, nf,
+                                  best, slot);
             S.finder[base + i] = slot;
         }
-    }
-    wave_sync();
-    // rows out: two lanes per agent, 16 B each
-    for (int q = lane; q < 2 * n; q += 64) {
-        const int i = q >> 1, half = q & 1;
-        const size_t r = (size_t)S.obsrow[base + i];
-        const uint4 v = reinterpret_cast<const uint4 *>(L.sem + i * kSensor)[half];
-        reinterpret_cast<uint4 *>(nxt.sem + r * kSensor)[half] = v;
-        if (depth) {
-            const uint4 d = reinterpret_cast<const uint4 *>(L.dep + i * kSensor)[half];
-            reinterpret_cast<uint4 *>(nxt.depth + r * kSensor)[half] = d;
-        }
+        wave_sync();
     }
 }
 

@@ -511,22 +511,38 @@ static void world_phase_c(orc_sim *s, uint32_t wi)
 /* ------------------------------------------------------------------------ */
 /* Sensor (Madrona RenderingSystem raycast; build-defined spec)*/
 /* ------------------------------------------------------------------------ */
-static inline int ray_box(float ox, float oy, float dx, float dy,
-                          float minx, float maxx, float miny, float maxy, float *t)
+/* Ray tests use one reciprocal per ray (inv_dx, inv_dy, inv_a) instead of a
+ * division per test: a build-defined choice of the (unpinned) raycast spec,
+ * DESIGN.md 3.6; the HIP kernel evaluates the identical expressions. */
+typedef struct { float ox, oy, dx, dy, inv_dx, inv_dy, a, inv_a; } orc_ray;
+
+static inline orc_ray make_ray(float ox, float oy, float dx, float dy)
+{
+    orc_ray r;
+    r.ox = ox; r.oy = oy; r.dx = dx; r.dy = dy;
+    r.inv_dx = dx != 0.0f ? 1.0f / dx : 0.0f;
+    r.inv_dy = dy != 0.0f ? 1.0f / dy : 0.0f;
+    r.a = dx * dx + dy * dy;
+    r.inv_a = 1.0f / r.a;
+    return r;
+}
+
+static inline int ray_box(const orc_ray *r, float minx, float maxx, float miny, float maxy,
+                          float *t)
 {
     float tn = -INFINITY, tf = INFINITY;
-    if (dx == 0.0f) {
-        if (ox < minx || ox > maxx) return 0;
+    if (r->dx == 0.0f) {
+        if (r->ox < minx || r->ox > maxx) return 0;
     } else {
-        float t1 = (minx - ox) / dx, t2 = (maxx - ox) / dx;
+        float t1 = (minx - r->ox) * r->inv_dx, t2 = (maxx - r->ox) * r->inv_dx;
         if (t1 > t2) { float q = t1; t1 = t2; t2 = q; }
         tn = fmax_std(tn, t1);
         tf = fmin_std(tf, t2);
     }
-    if (dy == 0.0f) {
-        if (oy < miny || oy > maxy) return 0;
+    if (r->dy == 0.0f) {
+        if (r->oy < miny || r->oy > maxy) return 0;
     } else {
-        float t1 = (miny - oy) / dy, t2 = (maxy - oy) / dy;
+        float t1 = (miny - r->oy) * r->inv_dy, t2 = (maxy - r->oy) * r->inv_dy;
         if (t1 > t2) { float q = t1; t1 = t2; t2 = q; }
         tn = fmax_std(tn, t1);
         tf = fmin_std(tf, t2);
@@ -536,18 +552,18 @@ static inline int ray_box(float ox, float oy, float dx, float dy,
     return 1;
 }
 
-static inline int ray_circle(float ox, float oy, float dx, float dy, float cx, float cy, float *t)
+/* unit circle (agent_render.obj icosphere, radius ~1) */
+static inline int ray_circle(const orc_ray *r, float cx, float cy, float *t)
 {
-    float px = ox - cx, py = oy - cy;
-    float a = dx * dx + dy * dy;
-    float b = px * dx + py * dy;
+    float px = r->ox - cx, py = r->oy - cy;
+    float b = px * r->dx + py * r->dy;
     float c = (px * px + py * py) - 1.0f;
-    float disc = b * b - a * c;
+    float disc = b * b - r->a * c;
     if (disc < 0.0f) return 0;
     float sq = sqrtf(disc);
-    float t2 = (-b + sq) / a;
+    float t2 = (-b + sq) * r->inv_a;
     if (t2 < 0.0f) return 0;
-    float t1 = (-b - sq) / a;
+    float t1 = (-b - sq) * r->inv_a;
     *t = t1 > 0.0f ? t1 : 0.0f;
     return 1;
 }
@@ -561,16 +577,19 @@ static const float kWall[4][4] = {
     {128.0f - 0.2f, 128.0f + 0.2f, 48.0f - 48.0f, 48.0f + 48.0f},
 };
 
-/* Cast one ray; returns semantic class, *t, and the agent slot hit (-1). */
+/* Cast one ray; returns semantic class, *t, and the agent slot hit (-1).
+ * Objects are tested in a fixed order -- walls, live food packages in
+ * (chunk, package) order, agents in slot order -- and a later object wins only
+ * with a strictly smaller t. */
 static int cast(const orc_world *w, int32_t self, float ox, float oy, float dx, float dy,
                 float *tbest, int32_t *hit_slot)
 {
+    const orc_ray ray = make_ray(ox, oy, dx, dy);
     float best = INFINITY, t;
     int sem = -1;
     int32_t slot = -1;
     for (int k = 0; k < 4; ++k) {
-        if (ray_box(ox, oy, dx, dy, kWall[k][0], kWall[k][1], kWall[k][2], kWall[k][3], &t) &&
-            t < best) {
+        if (ray_box(&ray, kWall[k][0], kWall[k][1], kWall[k][2], kWall[k][3], &t) && t < best) {
             best = t; sem = 5; slot = -1;
         }
     }
@@ -580,15 +599,14 @@ static int cast(const orc_world *w, int32_t self, float ox, float oy, float dx, 
         for (int k = 0; k < ORC_MAX_PKG; ++k) {
             if (w->pkg_n[c][k] == 0) continue;
             float fx = (float)w->pkg_x[c][k] + bx, fy = (float)w->pkg_y[c][k] + by;
-            if (ray_box(ox, oy, dx, dy, fx - 1.0f, fx + 1.0f, fy - 1.0f, fy + 1.0f, &t) &&
-                t < best) {
+            if (ray_box(&ray, fx - 1.0f, fx + 1.0f, fy - 1.0f, fy + 1.0f, &t) && t < best) {
                 best = t; sem = 6; slot = -1;
             }
         }
     }
     for (int32_t j = 0; j < w->n; ++j) {
         if (j == self) continue;
-        if (ray_circle(ox, oy, dx, dy, w->ag[j].x, w->ag[j].y, &t) && t < best) {
+        if (ray_circle(&ray, w->ag[j].x, w->ag[j].y, &t) && t < best) {
             best = t; sem = w->ag[j].species; slot = j;
         }
     }
