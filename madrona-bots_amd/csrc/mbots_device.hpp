@@ -89,67 +89,8 @@ __device__ __forceinline__ void heading(float w, float z, float &dx, float &dy)
 }
 
 // ---------------------------------------------------------------------------
-// Sensor primitives (build-defined raycast spec)
+// Sensor output quantisation
 // ---------------------------------------------------------------------------
-// One reciprocal per ray (inv_dx, inv_dy, inv_a) instead of a division per
-// test: the build's raycast spec; oracle/mbots_oracle.c evaluates the same
-// expressions in the same order.
-struct Ray {
-    float ox, oy, dx, dy, inv_dx, inv_dy, a, inv_a;
-};
-
-__device__ __forceinline__ Ray make_ray(float ox, float oy, float dx, float dy)
-{
-    Ray r;
-    r.ox = ox; r.oy = oy; r.dx = dx; r.dy = dy;
-    r.inv_dx = dx != 0.0f ? 1.0f / dx : 0.0f;
-    r.inv_dy = dy != 0.0f ? 1.0f / dy : 0.0f;
-    r.a = dx * dx + dy * dy;
-    r.inv_a = 1.0f / r.a;
-    return r;
-}
-
-__device__ __forceinline__ bool ray_box(const Ray &r, float minx, float maxx, float miny,
-                                        float maxy, float &t)
-{
-    float tn = -__builtin_inff(), tf = __builtin_inff();
-    if (r.dx == 0.0f) {
-        if (r.ox < minx || r.ox > maxx) return false;
-    } else {
-        float t1 = (minx - r.ox) * r.inv_dx, t2 = (maxx - r.ox) * r.inv_dx;
-        if (t1 > t2) { float q = t1; t1 = t2; t2 = q; }
-        tn = fmax_std(tn, t1);
-        tf = fmin_std(tf, t2);
-    }
-    if (r.dy == 0.0f) {
-        if (r.oy < miny || r.oy > maxy) return false;
-    } else {
-        float t1 = (miny - r.oy) * r.inv_dy, t2 = (maxy - r.oy) * r.inv_dy;
-        if (t1 > t2) { float q = t1; t1 = t2; t2 = q; }
-        tn = fmax_std(tn, t1);
-        tf = fmin_std(tf, t2);
-    }
-    if (tf < tn || tf < 0.0f) return false;
-    t = tn > 0.0f ? tn : 0.0f;
-    return true;
-}
-
-// unit circle (agent_render.obj icosphere, radius ~1)
-__device__ __forceinline__ bool ray_circle(const Ray &r, float cx, float cy, float &t)
-{
-    float px = r.ox - cx, py = r.oy - cy;
-    float b = px * r.dx + py * r.dy;
-    float c = (px * px + py * py) - 1.0f;
-    float disc = b * b - r.a * c;
-    if (disc < 0.0f) return false;
-    float sq = sqrtf(disc);
-    float t2 = (-b + sq) * r.inv_a;
-    if (t2 < 0.0f) return false;
-    float t1 = (-b - sq) * r.inv_a;
-    t = t1 > 0.0f ? t1 : 0.0f;
-    return true;
-}
-
 __device__ __forceinline__ uint8_t depth_u8(float t)
 {
     if (!(t < 255.0f)) return 255;

@@ -513,80 +513,191 @@ __global__ __launch_bounds__(256) void export_kernel(SimState S, ObsTable cur, O
 
 // ---------------------------------------------------------------------------
 // K4: sensor -- 32-pixel raycast (24 forward + 8 backward) plus the finder ray
-// (Madrona RenderingSystem, sim.cpp:1183-1188; spec DESIGN.md 3.6).
-// One wave per world.  Pass A culls every (agent, object) pair to the pixels
-// whose ray can reach the object's inflated bounding circle and records them
-// in per-(agent, pixel) candidate bitmasks in LDS; pass B casts each pixel's
-// ray exactly against the 4 walls and its candidates only, in the fixed object
-// order (food, then agents by slot) with strict '<' -- the same result as
-// testing every object.  Culling uses approximate math with margins; the exact
-// tests decide every hit.
+// (Madrona RenderingSystem, sim.cpp:1183-1188).  Build spec:
+// objects are unit circles; in an agent's frame (f along heading h, l along
+// r = (hy, -hx)) ray h + u r meets a circle iff
+//     q(u) = (A u - 2 l f) u + C <= 0,   A = f^2 - 1,  C = l^2 - 1,
+// ahead of the origin iff f + u l > 0 (backward camera: < 0); view depth
+// z = f - 1 (>= 0); walls: the ray's exit from the inner arena rectangle.
+// Each ray takes the lexicographic minimum of (z, order) with order = wall 0,
+// food 1 + k, agents 64 + slot.
+//
+// One wave per world, agents in chunks of kKeyAgents:
+//  A1  flattened (agent, object) pairs; a wedge test |l| <= |f| + sqrt(2)
+//      (necessary for any hit with |u| < 1) compacts survivors into a queue;
+//  A2  per survivor: approximate roots of q bound the candidate pixels; the
+//      exact predicate runs on those only and ds_min_u64's (z_bits, order)
+//      into the ray key.  Objects that cover many pixels (near, or |f| small)
+//      are evaluated on all 33 rays by the whole wave;
+//  out per (agent, ray): wall depth vs key -> semantic / depth bytes, finder.
+// The exact predicate and depths are evaluated with the same float
+// expressions as oracle/mbots_oracle.c; culling only skips rays it proves
+// cannot pass the predicate.
 // ---------------------------------------------------------------------------
-constexpr int kMaskWords = 1152;              // 4.5 KiB of candidate masks per world
+constexpr int kKeyAgents = 8;                 // agents per chunk (key rows)
+constexpr int kQueue = 128;                   // survivor queue entries
 constexpr int kMaxFood = kFoodCap + 2;        // live packages == currentNumFood <= 30
-constexpr float kRCircle = 1.0f + 0.05f;      // cull radius of a unit circle
-constexpr float kRBox = 1.41421356f + 0.05f;  // cull radius of a unit half-extent box
-constexpr float kNearPad = 0.5f;              // |f| <= R + pad: every pixel
+constexpr float kWedge = 1.41421356f + 0.05f; // |l| <= |f| + sqrt(2) (+ margin)
+constexpr float kUEps = 2e-3f;                // root-interval margin in u
+constexpr uint32_t kOrderFood = 1u;           // object order: wall 0, food 1.., agents 64..
+constexpr uint32_t kOrderAgent = 64u;
+constexpr unsigned long long kNoHit = ~0ull;
 
 struct SensorLDS {
     float ox[kMaxFood + kMaxCap], oy[kMaxFood + kMaxCap];   // food then agents
     float hx[kMaxCap], hy[kMaxCap];
     int32_t sp[kMaxCap];
-    uint32_t mask[kMaskWords];
+    unsigned long long key[kKeyAgents * kRays];
+    uint32_t queue[kQueue];
+    float u[kSensor];
 };
 
-__constant__ float kWallBox[4][4] = {
-    {64.0f - 64.0f, 64.0f + 64.0f, 0.0f - 0.2f, 0.0f + 0.2f},
-    {0.0f - 0.2f, 0.0f + 0.2f, 48.0f - 48.0f, 48.0f + 48.0f},
-    {64.0f - 64.0f, 64.0f + 64.0f, 96.0f - 0.2f, 96.0f + 0.2f},
-    {128.0f - 0.2f, 128.0f + 0.2f, 48.0f - 48.0f, 48.0f + 48.0f},
-};
+constexpr float kInLo = 0.0f + 0.2f;          // inner arena rectangle (walls, sim.cpp:157-194)
+constexpr float kInHiX = 128.0f - 0.2f;
+constexpr float kInHiY = 96.0f - 0.2f;
 
-__device__ __forceinline__ int clamp_floor(float v, int lo, int hi)
+// pinhole offsets (IEEE constant folding == the oracle's runtime division)
+constexpr float u_of(int k)
 {
-    v = fminf(fmaxf(v, (float)lo - 1.0f), (float)hi + 1.0f);
-    return (int)floorf(v);
+    return k < 24 ? (float)(2 * k + 1) / 24.0f - 1.0f : (float)(2 * (k - 24) + 1) / 8.0f - 1.0f;
 }
-__device__ __forceinline__ int clamp_ceil(float v, int lo, int hi)
+#define MB_U4(k) u_of(k), u_of(k + 1), u_of(k + 2), u_of(k + 3)
+__constant__ float kURay[kSensor] = {MB_U4(0),  MB_U4(4),  MB_U4(8),  MB_U4(12),
+                                     MB_U4(16), MB_U4(20), MB_U4(24), MB_U4(28)};
+#undef MB_U4
+
+__device__ __forceinline__ float max0(float x) { return x > 0.0f ? x : 0.0f; }
+
+__device__ __forceinline__ unsigned long long make_key(float z, uint32_t order)
 {
-    v = fminf(fmaxf(v, (float)lo - 1.0f), (float)hi + 1.0f);
-    return (int)ceilf(v);
+    return ((unsigned long long)__float_as_uint(z) << 32) | order;
 }
 
-// exact cast of one ray against walls + candidate bitmask (object order)
-__device__ __forceinline__ int cast_candidates(const SensorLDS &L, const Ray &ray,
-                                               const uint32_t *mk, int words, int nf,
-                                               float &best, int &slot)
+// wall depth of ray k: exit from the inner rectangle; 0 inside a wall box
+__device__ __forceinline__ float wall_z(const SensorLDS &L, int k, float ox, float oy, float hx,
+                                        float hy)
 {
-    best = __builtin_inff();
-    int sem = -1;
-    slot = -1;
-    float t;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        if (ray_box(ray, kWallBox[k][0], kWallBox[k][1], kWallBox[k][2], kWallBox[k][3], t) &&
-            t < best) {
-            best = t; sem = 5; slot = -1;
-        }
+    float dx, dy;
+    if (k < 24) {
+        const float u = L.u[k];
+        dx = hx + u * hy;
+        dy = hy + u * (-hx);
+    } else if (k < kSensor) {
+        const float u = L.u[k];
+        dx = -(hx + u * hy);
+        dy = -(hy + u * (-hx));
+    } else {
+        dx = hx;
+        dy = hy;
     }
-    for (int wd = 0; wd < words; ++wd) {
-        uint32_t m = mk[wd];
-        while (m) {
-            const int j = wd * 32 + __builtin_ctz(m);
-            m &= m - 1u;
-            const float cx = L.ox[j], cy = L.oy[j];
-            if (j < nf) {
-                if (ray_box(ray, cx - 1.0f, cx + 1.0f, cy - 1.0f, cy + 1.0f, t) && t < best) {
-                    best = t; sem = 6; slot = -1;
-                }
+    if (!(ox >= kInLo && ox <= kInHiX && oy >= kInLo && oy <= kInHiY)) return 0.0f;
+    float tx = __builtin_inff(), ty = __builtin_inff();
+    if (dx > 0.0f) tx = (kInHiX - ox) / dx;
+    else if (dx < 0.0f) tx = (kInLo - ox) / dx;
+    if (dy > 0.0f) ty = (kInHiY - oy) / dy;
+    else if (dy < 0.0f) ty = (kInLo - oy) / dy;
+    const float t = fmin_std(tx, ty);
+    return t == 0.0f ? 0.0f : t;
+}
+
+// exact predicate of object (f, l) on ray k; returns the key or kNoHit
+__device__ __forceinline__ unsigned long long ray_hit(const SensorLDS &L, int k, float f, float l,
+                                                      float A, float B2, float C, uint32_t order)
+{
+    if (k < kSensor) {
+        const float u = L.u[k];
+        const float q = (A * u - B2) * u + C;
+        const float p = f + u * l;
+        if (q <= 0.0f) {
+            if (k < 24) { if (p > 0.0f) return make_key(max0(f - 1.0f), order); }
+            else if (p < 0.0f) return make_key(max0(-f - 1.0f), order);
+        }
+        return kNoHit;
+    }
+    if (C <= 0.0f && f > 0.0f) return make_key(max0(f - 1.0f), order);
+    return kNoHit;
+}
+
+__device__ __forceinline__ void pair_frame(const SensorLDS &L, int nf, int i, int j, float &f,
+                                           float &l)
+{
+    const float vx = L.ox[j] - L.ox[nf + i], vy = L.oy[j] - L.oy[nf + i];
+    const float hx = L.hx[i], hy = L.hy[i];
+    f = vx * hx + vy * hy;
+    l = vx * hy - vy * hx;
+}
+
+// A2 over queue entries [q0, q0 + cnt) (cnt <= 64)
+__device__ __forceinline__ void process_queue(SensorLDS &L, int a0, int nf, int q0, int cnt)
+{
+    const int lane = (int)__lane_id();
+    bool wide = false;
+    float f = 0.f, l = 0.f, A = 0.f, B2 = 0.f, C = 0.f;
+    uint32_t order = 0, ii = 0;
+    if (lane < cnt) {
+        const uint32_t e = L.queue[q0 + lane];
+        ii = e & 0xFFu;
+        const int j = (int)(e >> 8);
+        order = j < nf ? kOrderFood + (uint32_t)j : kOrderAgent + (uint32_t)(j - nf);
+        pair_frame(L, nf, a0 + (int)ii, j, f, l);
+        const float r2 = f * f + l * l;
+        A = f * f - 1.0f;
+        B2 = 2.0f * (l * f);
+        C = l * l - 1.0f;
+        unsigned long long *key = L.key + ii * kRays;
+        if (r2 <= 1.0f || fabsf(f) <= 1.5f) {
+            wide = true;
+        } else {
+            // approximate roots of q bound the candidate pixels
+            const float sq = __builtin_amdgcn_sqrtf(r2 - 1.0f);
+            const float ia = __builtin_amdgcn_rcpf(A);
+            const float u1 = (l * f - sq) * ia - kUEps, u2 = (l * f + sq) * ia + kUEps;
+            int k0, k1;
+            if (f > 0.0f) {
+                k0 = (int)ceilf(fmaxf((u1 + 1.0f) * 12.0f - 0.5f, -1.0f));
+                k1 = (int)floorf(fminf((u2 + 1.0f) * 12.0f - 0.5f, 24.0f));
+                k0 = max(k0, 0);
+                k1 = min(k1, 23);
             } else {
-                if (ray_circle(ray, cx, cy, t) && t < best) {
-                    best = t; sem = L.sp[j - nf]; slot = j - nf;
+                k0 = (int)ceilf(fmaxf((u1 + 1.0f) * 4.0f - 0.5f, -1.0f));
+                k1 = (int)floorf(fminf((u2 + 1.0f) * 4.0f - 0.5f, 8.0f));
+                k0 = 24 + max(k0, 0);
+                k1 = 24 + min(k1, 7);
+            }
+            const int c = k1 - k0 + 1;
+            if (c > 3) {
+                wide = true;
+            } else {
+#pragma unroll
+                for (int e2 = 0; e2 < 3; ++e2) {
+                    if (e2 < c) {
+                        const unsigned long long kv = ray_hit(L, k0 + e2, f, l, A, B2, C, order);
+                        if (kv != kNoHit) atomicMin(&key[k0 + e2], kv);
+                    }
+                }
+                if (f > 0.0f && u1 <= 0.0f && u2 >= 0.0f) {
+                    const unsigned long long kv = ray_hit(L, kSensor, f, l, A, B2, C, order);
+                    if (kv != kNoHit) atomicMin(&key[kSensor], kv);
                 }
             }
         }
     }
-    return sem;
+    // wide objects: the whole wave evaluates all 33 rays of each
+    uint64_t wm = ballot64(wide);
+    while (wm) {
+        const int src = __builtin_ctzll(wm);
+        wm &= wm - 1;
+        const float wf = __shfl(f, src), wl = __shfl(l, src);
+        const float wA = __shfl(A, src), wB2 = __shfl(B2, src), wC = __shfl(C, src);
+        const uint32_t word = (uint32_t)__shfl((int)order, src);
+        const uint32_t wii = (uint32_t)__shfl((int)ii, src);
+        const float r2 = wf * wf + wl * wl;
+        if (lane <= kSensor) {
+            const unsigned long long kv = r2 <= 1.0f ? make_key(0.0f, word)
+                                                     : ray_hit(L, lane, wf, wl, wA, wB2, wC, word);
+            if (kv != kNoHit) atomicMin(&L.key[wii * kRays + lane], kv);
+        }
+    }
 }
 
 __global__ __launch_bounds__(256) void sensor_kernel(SimState S, ObsTable nxt)
@@ -600,6 +711,7 @@ __global__ __launch_bounds__(256) void sensor_kernel(SimState S, ObsTable nxt)
     const size_t base = (size_t)w * S.cap;
     const int n = S.n[w];
     const bool depth = (S.flags & kFlagFixDepth) != 0;
+    if (lane < kSensor) L.u[lane] = kURay[lane];
 
     // live food packages in (chunk, package) order -> objects [0, nf)
     int nf = 0;
@@ -610,12 +722,10 @@ __global__ __launch_bounds__(256) void sensor_kernel(SimState S, ObsTable nxt)
         const uint64_t m = ballot64(live);
         if (live) {
             const int c = k / kMaxPkg;
-            const float bx = (float)((c % kChunksX) * kChunkW);
-            const float by = (float)((c / kChunksX) * kChunkW);
             const int s = nf + (int)rank_below(m);
             if (s < kMaxFood) {   // live packages == currentNumFood <= 30 (addFoodSystem)
-                L.ox[s] = (float)(p & 0xFFu) + bx;
-                L.oy[s] = (float)((p >> 8) & 0xFFu) + by;
+                L.ox[s] = (float)(p & 0xFFu) + (float)((c % kChunksX) * kChunkW);
+                L.oy[s] = (float)((p >> 8) & 0xFFu) + (float)((c / kChunksX) * kChunkW);
             }
         }
         nf += __popcll(m);
@@ -632,100 +742,58 @@ __global__ __launch_bounds__(256) void sensor_kernel(SimState S, ObsTable nxt)
         L.hy[i] = dy;
     }
     const int nobj = nf + n;
-    const int words = (nobj + 31) >> 5;
-    const int per_agent = kRays * words;
-    const int chunk = max(1, min(n, kMaskWords / per_agent));
     wave_sync();
 
-    for (int a0 = 0; a0 < n; a0 += chunk) {
-        const int nc = min(chunk, n - a0);
-        for (int q = lane; q < nc * per_agent; q += 64) L.mask[q] = 0u;
+    for (int a0 = 0; a0 < n; a0 += kKeyAgents) {
+        const int nc = min(kKeyAgents, n - a0);
+        for (int q = lane; q < nc * kRays; q += 64) L.key[q] = kNoHit;
         wave_sync();
-        // ---- pass A: (agent, object) -> candidate pixels ----
-        for (int ii = 0; ii < nc; ++ii) {
-            const int i = a0 + ii;
-            const float ax = L.ox[nf + i], ay = L.oy[nf + i], hx = L.hx[i], hy = L.hy[i];
-            uint32_t *mk = L.mask + ii * per_agent;
-            for (int j = lane; j < nobj; j += 64) {
-                if (j == nf + i) continue;   // no self hits
-                const float R = j < nf ? kRBox : kRCircle;
-                const float vx = L.ox[j] - ax, vy = L.oy[j] - ay;
-                const float f = vx * hx + vy * hy;   // along the heading
-                const float l = vx * hy - vy * hx;   // along r = (hy, -hx)
-                int plo = 0, phi = 23, blo = 0, bhi = 7;
-                bool fwd, bwd, fnd;
-                const float af = fabsf(f), al = fabsf(l);
-                if (af > R + kNearPad) {
-                    // bounding circle wholly in front / behind: pixel interval from
-                    // (l - u f)^2 <= R^2 (1 + u^2)  (ray direction d + u r)
-                    const float A = f * f - R * R;
-                    const float s = __builtin_amdgcn_sqrtf(f * f + l * l - R * R);
-                    const float ia = __builtin_amdgcn_rcpf(A);
-                    const float u1 = (l * f - R * s) * ia, u2 = (l * f + R * s) * ia;
-                    if (f > 0.0f) {
-                        bwd = false;
-                        plo = clamp_ceil((u1 + 1.0f) * 12.0f - 0.5f - 0.02f, 0, 23);
-                        phi = clamp_floor((u2 + 1.0f) * 12.0f - 0.5f + 0.02f, 0, 23);
-                        fwd = plo <= phi;
-                        fnd = (u1 - 1e-3f <= 0.0f) && (u2 + 1e-3f >= 0.0f);
-                    } else {
-                        fwd = false;
-                        fnd = false;
-                        blo = clamp_ceil((u1 + 1.0f) * 4.0f - 0.5f - 0.02f, 0, 7);
-                        bhi = clamp_floor((u2 + 1.0f) * 4.0f - 0.5f + 0.02f, 0, 7);
-                        bwd = blo <= bhi;
-                    }
-                } else {
-                    // beside the agent: test against the 90-degree view wedges
-                    // |l| <= f (forward) and |l| <= -f (backward); every pixel of a
-                    // wedge the circle may touch
-                    const float lim = R * 1.41421356f + 0.05f;
-                    fwd = (al - f <= lim) && (f >= -R - 0.05f);
-                    bwd = (al + f <= lim) && (f <= R + 0.05f);
-                    fnd = (al <= R + 0.05f) && (f >= -R - 0.05f);
-                }
-                const uint32_t bit = 1u << (j & 31);
-                const int wd = j >> 5;
-                if (fwd) {
-                    for (int p = max(plo, 0); p <= min(phi, 23); ++p) atomicOr(&mk[p * words + wd], bit);
-                }
-                if (bwd) {
-                    for (int p = max(blo, 0); p <= min(bhi, 7); ++p)
-                        atomicOr(&mk[(24 + p) * words + wd], bit);
-                }
-                if (fnd) atomicOr(&mk[kSensor * words + wd], bit);
+        // ---- A1: wedge pre-cull of flattened pairs into the queue ----
+        int nq = 0;
+        int ii = 0, j = (int)lane;
+        while (j >= nobj) { j -= nobj; ++ii; }
+        const int npairs = nc * nobj;
+        for (int qb = 0; qb < npairs; qb += 64) {
+            bool keep = false;
+            if (ii < nc && j != nf + a0 + ii) {
+                float f, l;
+                pair_frame(L, nf, a0 + ii, j, f, l);
+                keep = fabsf(l) <= fabsf(f) + kWedge;
             }
+            const uint64_t m = ballot64(keep);
+            if (keep) L.queue[nq + (int)rank_below(m)] = (uint32_t)ii | ((uint32_t)j << 8);
+            nq += __popcll(m);
+            if (nq >= 64) {
+                wave_sync();
+                process_queue(L, a0, nf, nq - 64, 64);
+                wave_sync();
+                nq -= 64;
+            }
+            j += 64;
+            while (j >= nobj) { j -= nobj; ++ii; }
+        }
+        if (nq > 0) {
+            wave_sync();
+            process_queue(L, a0, nf, 0, nq);
         }
         wave_sync();
-        // ---- pass B: 32 pixel rays, two agents per wave ----
+        // ---- output: walls vs keys, two agents per wave ----
         for (int pb = 0; pb < nc; pb += 2) {
-            const int ii = pb + (int)(lane >> 5);
+            const int ci = pb + (int)(lane >> 5);
             const int px = (int)(lane & 31u);
-            const bool valid = ii < nc;
+            const bool valid = ci < nc;
             uint32_t semv = 0u, depv = 0u;
             if (valid) {
-                const int i = a0 + ii;
-                const float hx = L.hx[i], hy = L.hy[i];
-                const float rx = hy, ry = -hx;
-                float dx, dy;
-                if (px < 24) {
-                    const float u = (float)(2 * px + 1) / 24.0f - 1.0f;
-                    dx = hx + u * rx;
-                    dy = hy + u * ry;
-                } else {
-                    const float u = (float)(2 * (px - 24) + 1) / 8.0f - 1.0f;
-                    dx = -(hx + u * rx);
-                    dy = -(hy + u * ry);
-                }
-                const Ray ray = make_ray(L.ox[nf + i], L.oy[nf + i], dx, dy);
-                float best;
-                int slot;
-                const int sem = cast_candidates(L, ray, L.mask + ii * per_agent + px * words, words,
-                                                nf, best, slot);
+                const int i = a0 + ci;
+                const float wz = wall_z(L, px, L.ox[nf + i], L.oy[nf + i], L.hx[i], L.hy[i]);
+                unsigned long long kv = L.key[ci * kRays + px];
+                const unsigned long long kw = make_key(wz, 0u);
+                if (kw < kv) kv = kw;
+                const uint32_t order = (uint32_t)kv;
+                const int sem = order == 0u ? 5 : (order < kOrderAgent ? 6 : L.sp[order - kOrderAgent]);
                 semv = (uint32_t)(uint8_t)(int8_t)sem;
-                depv = depth_u8(best);
+                depv = depth_u8(__uint_as_float((uint32_t)(kv >> 32)));
             }
-            // pack 4 lanes' bytes into one dword and store 32-B rows
             semv <<= 8u * (lane & 3u);
             depv <<= 8u * (lane & 3u);
             semv |= __shfl_xor(semv, 1);
@@ -733,20 +801,19 @@ __global__ __launch_bounds__(256) void sensor_kernel(SimState S, ObsTable nxt)
             depv |= __shfl_xor(depv, 1);
             depv |= __shfl_xor(depv, 2);
             if (valid && (lane & 3u) == 0u) {
-                const size_t r = (size_t)S.obsrow[base + a0 + ii];
+                const size_t r = (size_t)S.obsrow[base + a0 + ci];
                 reinterpret_cast<uint32_t *>(nxt.sem + r * kSensor)[px >> 2] = semv;
                 if (depth) reinterpret_cast<uint32_t *>(nxt.depth + r * kSensor)[px >> 2] = depv;
             }
         }
-        // ---- finder ray (forward centre) ----
-        for (int ii = lane; ii < nc; ii += 64) {
-            const int i = a0 + ii;
-            const Ray ray = make_ray(L.ox[nf + i], L.oy[nf + i], L.hx[i], L.hy[i]);
-            float best;
-            int slot;
-            (void)cast_candidates(L, ray, L.mask + ii * per_agent + kSensor * words, words, nf,
-                                  best, slot);
-            S.finder[base + i] = slot;
+        if ((int)lane < nc) {
+            const int i = a0 + (int)lane;
+            const float wz = wall_z(L, kSensor, L.ox[nf + i], L.oy[nf + i], L.hx[i], L.hy[i]);
+            unsigned long long kv = L.key[lane * kRays + kSensor];
+            const unsigned long long kw = make_key(wz, 0u);
+            if (kw < kv) kv = kw;
+            const uint32_t order = (uint32_t)kv;
+            S.finder[base + i] = order >= kOrderAgent ? (int32_t)(order - kOrderAgent) : -1;
         }
         wave_sync();
     }

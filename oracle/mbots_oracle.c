@@ -510,109 +510,88 @@ static void world_phase_c(orc_sim *s, uint32_t wi)
 
 /* ------------------------------------------------------------------------ */
 /* Sensor (Madrona RenderingSystem raycast; build-defined spec)*/
+/*                                                                           */
+/* 32 pinhole pixels per agent (24 forward over the 90-degree FOV, 8 backward,*/
+/* gfx.cpp:252-253) plus the forward centre "finder" ray.  Every object (live */
+/* food package, other agent) is a unit circle; in the agent's frame (f along */
+/* the heading h, l along r = (hy, -hx)) the ray direction h + u r meets the  */
+/* circle iff q(u) = (A u - 2 l f) u + C <= 0 with A = f^2 - 1, C = l^2 - 1,  */
+/* and the hit lies ahead of the ray iff f + u l > 0 (backward camera: < 0).  */
+/* Depth is view-space z: z = f - 1 (clamped at 0) for circles, the ray's     */
+/* exit from the inner arena rectangle for the walls.  Each pixel takes the   */
+/* lexicographic minimum of (z, order): walls 0, food 1 + k, agents 64 + slot.*/
 /* ------------------------------------------------------------------------ */
-/* Ray tests use one reciprocal per ray (inv_dx, inv_dy, inv_a) instead of a
- * division per test: a build-defined choice of the (unpinned) raycast spec,
- * DESIGN.md 3.6; the HIP kernel evaluates the identical expressions. */
-typedef struct { float ox, oy, dx, dy, inv_dx, inv_dy, a, inv_a; } orc_ray;
+static const float kInLo = 0.0f + 0.2f;     /* walls: makeWalls (sim.cpp:157-194), */
+static const float kInHiX = 128.0f - 0.2f;  /* 0.2-thick boxes on the boundary    */
+static const float kInHiY = 96.0f - 0.2f;
 
-static inline orc_ray make_ray(float ox, float oy, float dx, float dy)
+static float ray_u(int k)
 {
-    orc_ray r;
-    r.ox = ox; r.oy = oy; r.dx = dx; r.dy = dy;
-    r.inv_dx = dx != 0.0f ? 1.0f / dx : 0.0f;
-    r.inv_dy = dy != 0.0f ? 1.0f / dy : 0.0f;
-    r.a = dx * dx + dy * dy;
-    r.inv_a = 1.0f / r.a;
-    return r;
+    if (k < 24) return (float)(2 * k + 1) / 24.0f - 1.0f;
+    return (float)(2 * (k - 24) + 1) / 8.0f - 1.0f;
 }
 
-static inline int ray_box(const orc_ray *r, float minx, float maxx, float miny, float maxy,
-                          float *t)
+/* ray direction k of heading (hx, hy) */
+static void ray_dir(int k, float hx, float hy, float *dx, float *dy)
 {
-    float tn = -INFINITY, tf = INFINITY;
-    if (r->dx == 0.0f) {
-        if (r->ox < minx || r->ox > maxx) return 0;
+    if (k < 24) {
+        float u = ray_u(k);
+        *dx = hx + u * hy;
+        *dy = hy + u * (-hx);
+    } else if (k < ORC_SENSOR) {
+        float u = ray_u(k);
+        *dx = -(hx + u * hy);
+        *dy = -(hy + u * (-hx));
     } else {
-        float t1 = (minx - r->ox) * r->inv_dx, t2 = (maxx - r->ox) * r->inv_dx;
-        if (t1 > t2) { float q = t1; t1 = t2; t2 = q; }
-        tn = fmax_std(tn, t1);
-        tf = fmin_std(tf, t2);
+        *dx = hx;
+        *dy = hy;
     }
-    if (r->dy == 0.0f) {
-        if (r->oy < miny || r->oy > maxy) return 0;
-    } else {
-        float t1 = (miny - r->oy) * r->inv_dy, t2 = (maxy - r->oy) * r->inv_dy;
-        if (t1 > t2) { float q = t1; t1 = t2; t2 = q; }
-        tn = fmax_std(tn, t1);
-        tf = fmin_std(tf, t2);
-    }
-    if (tf < tn || tf < 0.0f) return 0;
-    *t = tn > 0.0f ? tn : 0.0f;
-    return 1;
 }
 
-/* unit circle (agent_render.obj icosphere, radius ~1) */
-static inline int ray_circle(const orc_ray *r, float cx, float cy, float *t)
+/* wall depth: exit from the inner rectangle; 0 if the origin is in a wall box */
+static float wall_z(float ox, float oy, float dx, float dy)
 {
-    float px = r->ox - cx, py = r->oy - cy;
-    float b = px * r->dx + py * r->dy;
-    float c = (px * px + py * py) - 1.0f;
-    float disc = b * b - r->a * c;
-    if (disc < 0.0f) return 0;
-    float sq = sqrtf(disc);
-    float t2 = (-b + sq) * r->inv_a;
-    if (t2 < 0.0f) return 0;
-    float t1 = (-b - sq) * r->inv_a;
-    *t = t1 > 0.0f ? t1 : 0.0f;
-    return 1;
+    if (!(ox >= kInLo && ox <= kInHiX && oy >= kInLo && oy <= kInHiY)) return 0.0f;
+    float tx = INFINITY, ty = INFINITY;
+    if (dx > 0.0f) tx = (kInHiX - ox) / dx;
+    else if (dx < 0.0f) tx = (kInLo - ox) / dx;
+    if (dy > 0.0f) ty = (kInHiY - oy) / dy;
+    else if (dy < 0.0f) ty = (kInLo - oy) / dy;
+    float t = fmin_std(tx, ty);
+    return t == 0.0f ? 0.0f : t;
 }
 
-/* walls: makeWalls (sim.cpp:157-194): centroid +- scale */
-static const float kWall[4][4] = {
-    /* minx, maxx, miny, maxy */
-    {64.0f - 64.0f, 64.0f + 64.0f, 0.0f - 0.2f, 0.0f + 0.2f},
-    {0.0f - 0.2f, 0.0f + 0.2f, 48.0f - 48.0f, 48.0f + 48.0f},
-    {64.0f - 64.0f, 64.0f + 64.0f, 96.0f - 0.2f, 96.0f + 0.2f},
-    {128.0f - 0.2f, 128.0f + 0.2f, 48.0f - 48.0f, 48.0f + 48.0f},
-};
+static inline float max0(float x) { return x > 0.0f ? x : 0.0f; }
 
-/* Cast one ray; returns semantic class, *t, and the agent slot hit (-1).
- * Objects are tested in a fixed order -- walls, live food packages in
- * (chunk, package) order, agents in slot order -- and a later object wins only
- * with a strictly smaller t. */
-static int cast(const orc_world *w, int32_t self, float ox, float oy, float dx, float dy,
-                float *tbest, int32_t *hit_slot)
+typedef struct { float z; uint32_t order; } orc_hit;
+
+static inline void consider(orc_hit *h, float z, uint32_t order)
 {
-    const orc_ray ray = make_ray(ox, oy, dx, dy);
-    float best = INFINITY, t;
-    int sem = -1;
-    int32_t slot = -1;
-    for (int k = 0; k < 4; ++k) {
-        if (ray_box(&ray, kWall[k][0], kWall[k][1], kWall[k][2], kWall[k][3], &t) && t < best) {
-            best = t; sem = 5; slot = -1;
-        }
+    if (z < h->z || (z == h->z && order < h->order)) { h->z = z; h->order = order; }
+}
+
+/* one object (unit circle at (cx, cy)) against all 33 rays of an agent */
+static void raster(orc_hit *hits, float ax, float ay, float hx, float hy, float cx, float cy,
+                   uint32_t order)
+{
+    float vx = cx - ax, vy = cy - ay;
+    float f = vx * hx + vy * hy;
+    float l = vx * hy - vy * hx;
+    float r2 = f * f + l * l;
+    if (r2 <= 1.0f) {
+        for (int k = 0; k <= ORC_SENSOR; ++k) consider(&hits[k], 0.0f, order);
+        return;
     }
-    for (int c = 0; c < ORC_NUM_CHUNKS; ++c) {
-        float bx = (float)((c % ORC_CHUNKS_X) * ORC_CHUNK_W);
-        float by = (float)((c / ORC_CHUNKS_X) * ORC_CHUNK_W);
-        for (int k = 0; k < ORC_MAX_PKG; ++k) {
-            if (w->pkg_n[c][k] == 0) continue;
-            float fx = (float)w->pkg_x[c][k] + bx, fy = (float)w->pkg_y[c][k] + by;
-            if (ray_box(&ray, fx - 1.0f, fx + 1.0f, fy - 1.0f, fy + 1.0f, &t) && t < best) {
-                best = t; sem = 6; slot = -1;
-            }
-        }
+    float A = f * f - 1.0f, B2 = 2.0f * (l * f), C = l * l - 1.0f;
+    for (int k = 0; k < ORC_SENSOR; ++k) {
+        float u = ray_u(k);
+        float q = (A * u - B2) * u + C;
+        float p = f + u * l;
+        if (!(q <= 0.0f)) continue;
+        if (k < 24) { if (p > 0.0f) consider(&hits[k], max0(f - 1.0f), order); }
+        else { if (p < 0.0f) consider(&hits[k], max0(-f - 1.0f), order); }
     }
-    for (int32_t j = 0; j < w->n; ++j) {
-        if (j == self) continue;
-        if (ray_circle(&ray, w->ag[j].x, w->ag[j].y, &t) && t < best) {
-            best = t; sem = w->ag[j].species; slot = j;
-        }
-    }
-    *tbest = best;
-    *hit_slot = slot;
-    return sem;
+    if (C <= 0.0f && f > 0.0f) consider(&hits[ORC_SENSOR], max0(f - 1.0f), order);
 }
 
 static inline uint8_t depth_u8(float t)
@@ -625,31 +604,40 @@ static void world_phase_d(orc_sim *s, uint32_t wi)
 {
     orc_world *w = &s->w[wi];
     orc_cols *nc = &s->cur[s->tb ^ 1];
+    orc_hit hits[ORC_SENSOR + 1];
     for (int32_t i = 0; i < w->n; ++i) {
         orc_agent *a = &w->ag[i];
-        float dx, dy, t;
-        int32_t hs;
-        heading(a->rw, a->rz, &dx, &dy);
-        float rx = dy, ry = -dx;   /* right vector */
+        float hx, hy;
+        heading(a->rw, a->rz, &hx, &hy);
+        for (int k = 0; k <= ORC_SENSOR; ++k) {
+            float dx, dy;
+            ray_dir(k, hx, hy, &dx, &dy);
+            hits[k].z = wall_z(a->x, a->y, dx, dy);
+            hits[k].order = 0;
+        }
+        uint32_t nf = 0;
+        for (int c = 0; c < ORC_NUM_CHUNKS; ++c) {
+            float bx = (float)((c % ORC_CHUNKS_X) * ORC_CHUNK_W);
+            float by = (float)((c / ORC_CHUNKS_X) * ORC_CHUNK_W);
+            for (int k = 0; k < ORC_MAX_PKG; ++k) {
+                if (w->pkg_n[c][k] == 0) continue;
+                float fx = (float)w->pkg_x[c][k] + bx, fy = (float)w->pkg_y[c][k] + by;
+                raster(hits, a->x, a->y, hx, hy, fx, fy, 1u + nf);
+                nf += 1;
+            }
+        }
+        for (int32_t j = 0; j < w->n; ++j) {
+            if (j == i) continue;
+            raster(hits, a->x, a->y, hx, hy, w->ag[j].x, w->ag[j].y, 64u + (uint32_t)j);
+        }
         int8_t *sem = nc->sem + (size_t)a->obs_row * ORC_SENSOR;
         uint8_t *dep = nc->depth + (size_t)a->obs_row * ORC_SENSOR;
-        for (int p = 0; p < ORC_SENSOR; ++p) {
-            float rdx, rdy;
-            if (p < 24) {
-                float u = (float)(2 * p + 1) / 24.0f - 1.0f;
-                rdx = dx + u * rx;
-                rdy = dy + u * ry;
-            } else {
-                float u = (float)(2 * (p - 24) + 1) / 8.0f - 1.0f;
-                rdx = -(dx + u * rx);
-                rdy = -(dy + u * ry);
-            }
-            int c = cast(w, i, a->x, a->y, rdx, rdy, &t, &hs);
-            sem[p] = (int8_t)c;
-            dep[p] = depth_u8(t);
+        for (int k = 0; k < ORC_SENSOR; ++k) {
+            uint32_t o = hits[k].order;
+            sem[k] = (int8_t)(o == 0 ? 5 : (o < 64 ? 6 : w->ag[o - 64].species));
+            dep[k] = depth_u8(hits[k].z);
         }
-        cast(w, i, a->x, a->y, dx, dy, &t, &hs);
-        a->finder = hs;
+        a->finder = hits[ORC_SENSOR].order >= 64 ? (int32_t)(hits[ORC_SENSOR].order - 64) : -1;
     }
 }
 
