@@ -1,14 +1,47 @@
 // mbots_kernels.hip -- hand-written gfx950 kernels of the per-step ECS sweep.
 //
 // Layout: agent state is SoA, [world][slot] with a
-// per-world slot capacity `cap`; one wave64 owns one world for the ECS
-// systems (4 worlds per 256-thread workgroup, no cross-wave sync), staging the
-// world's agents, chunk counters and food packages in LDS.  The exported
-// observation table is species-major (species, world, slot) and is written
-// into the other half of a double-buffered table every step.
+// per-world slot capacity `cap`; one wave64 owns one world (4 worlds per
+// 256-thread workgroup, waves never wait on each other except at the very end
+// of K1), staging the world in LDS.  The exported observation table is
+// species-major (species, world, slot) and written into the other half of a
+// double-buffered table every step.
+//
+// Step = K1 world_step (ECS systems + per-world compaction + per-tile species
+// counts) -> K2 scan (species-major row offsets) -> K3 export_sensor (row move,
+// observations, reward, raycast sensor) ; shift_observations = K5 shift.
 #include "mbots_kernels.hpp"
 
 namespace mbots {
+
+constexpr int kWorldsPerBlock = 4;
+constexpr int kTileWorlds = 1024;             // worlds per scan tile (K2 block)
+
+// ---------------------------------------------------------------------------
+// Food packages: HBM keeps one 8-byte record per chunk (5 x (x | y << 4) bytes,
+// live mask in byte 5: kMaxFoodPerPackage = 1, so numFood is a bit);
+// LDS keeps one u32 per package: x | y << 8 | numFood << 16.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void food_unpack(uint64_t rec, uint32_t *pk)
+{
+#pragma unroll
+    for (int k = 0; k < kMaxPkg; ++k) {
+        const uint32_t xy = (uint32_t)(rec >> (8 * k)) & 0xFFu;
+        const uint32_t live = (uint32_t)(rec >> (40 + k)) & 1u;
+        pk[k] = (xy & 15u) | ((xy >> 4) << 8) | (live << 16);
+    }
+}
+__device__ __forceinline__ uint64_t food_pack(const uint32_t *pk)
+{
+    uint64_t rec = 0;
+#pragma unroll
+    for (int k = 0; k < kMaxPkg; ++k) {
+        const uint32_t p = pk[k];
+        rec |= (uint64_t)((p & 15u) | (((p >> 8) & 15u) << 4)) << (8 * k);
+        rec |= (uint64_t)((p >> 16) & 1u) << (40 + k);
+    }
+    return rec;
+}
 
 // ---------------------------------------------------------------------------
 // Per-world LDS image used by the world-step kernel
@@ -36,7 +69,6 @@ constexpr uint32_t F_ALIVE = 1u << 4;
 constexpr uint32_t F_BREED = 1u << 5;
 constexpr uint32_t F_STATS = 0xFu;
 
-constexpr int kWorldsPerBlock = 4;
 
 __device__ __forceinline__ uint32_t rng_draw(uint2 key, uint32_t ctr)
 {
@@ -65,14 +97,34 @@ __device__ __forceinline__ void init_slot(WorldLDS &L, int s, float x, float y, 
 // speciesInfoSync + respawn, and the per-world compaction of
 // SortArchetypeNode<Agent, WorldID> (sim.cpp:1061-1132).
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void world_step_kernel(SimState S, ObsTable cur)
+__device__ void world_step(SimState &S, const ObsTable &cur, WorldLDS &L, uint32_t w,
+                           uint32_t lane);
+
+__global__ __launch_bounds__(256) void world_step_kernel(SimState S, ObsTable cur, int parity)
 {
     __shared__ WorldLDS lds[kWorldsPerBlock];
+    __shared__ int32_t blk[kWorldsPerBlock][5];
     const uint32_t wv = threadIdx.x >> 6;
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t w = blockIdx.x * kWorldsPerBlock + wv;
-    if (w >= S.W) return;
-    WorldLDS &L = lds[wv];
+    if (w < S.W) world_step(S, cur, lds[wv], w, lane);
+    // per-block species/agent counts -> the K2 scan tile (one atomic per counter)
+    if (lane < 5) {
+        const int32_t *sc = lds[wv].scount;
+        blk[wv][lane] = (w < S.W) ? (lane < 4 ? sc[lane] : sc[0] + sc[1] + sc[2] + sc[3]) : 0;
+    }
+    __syncthreads();
+    if (threadIdx.x < 5) {
+        const int32_t v = blk[0][threadIdx.x] + blk[1][threadIdx.x] + blk[2][threadIdx.x] +
+                          blk[3][threadIdx.x];
+        const uint32_t tile = (blockIdx.x * kWorldsPerBlock) / kTileWorlds;
+        atomicAdd(&S.tiles[(size_t)parity * S.ntiles * 5 + tile * 5 + threadIdx.x], v);
+    }
+}
+
+__device__ void world_step(SimState &S, const ObsTable &cur, WorldLDS &L, uint32_t w,
+                           uint32_t lane)
+{
     const uint32_t cap = S.cap;
     const size_t base = (size_t)w * cap;
     const int n0 = S.n[w];
@@ -89,7 +141,7 @@ __global__ __launch_bounds__(256) void world_step_kernel(SimState S, ObsTable cu
         L.obsrow[i] = S.obsrow[base + i];
         L.flags[i] = F_ALIVE;
     }
-    for (int k = lane; k < kNumPkg; k += 64) L.food[k] = S.food[(size_t)w * kNumPkg + k];
+    if (lane < kNumChunks) food_unpack(S.food[(size_t)w * kNumChunks + lane], &L.food[lane * kMaxPkg]);
     if (lane < kNumChunks) { L.nag[lane] = 0u; L.spd[lane] = 0u; }   // resetChunkInfoSystem
     if (lane < kNumSpecies) { L.cnt[lane] = 0u; L.hsum[lane] = 0u; L.scount[lane] = 0; }
     if (lane == 0) L.consumed = 0;
@@ -327,7 +379,7 @@ __global__ __launch_bounds__(256) void world_step_kernel(SimState S, ObsTable cu
         }
         nn += __popcll(m);
     }
-    for (int k = lane; k < kNumPkg; k += 64) S.food[(size_t)w * kNumPkg + k] = L.food[k];
+    if (lane < kNumChunks) S.food[(size_t)w * kNumChunks + lane] = food_pack(&L.food[lane * kMaxPkg]);
     wave_sync();
     if (lane < kNumSpecies) S.scount[(size_t)w * kNumSpecies + lane] = L.scount[lane];
     if (lane == 0) {
@@ -339,180 +391,110 @@ __global__ __launch_bounds__(256) void world_step_kernel(SimState S, ObsTable cu
 }
 
 // ---------------------------------------------------------------------------
-// K2: species-major row offsets.  row_base[w][s] = sum_{s'<s} total[s'] +
-// sum_{w'<w} count[w'][s]  (SortArchetypeNode<Obs, SpeciesObservation>,
-// sim.cpp:1147-1149, made deterministic); world_off[w] for agentOffsetForWorld.
-// One 1024-thread workgroup.
+// K2: species-major row offsets (SortArchetypeNode<Obs, SpeciesObservation>,
+// sim.cpp:1147-1149, made deterministic: rows ordered by (species, world,
+// slot)).  row_base[w][s] = sum_{s'<s} total[s'] + sum_{w'<w} count[w'][s];
+// world_off[w] = sum_{w'<w} n[w'] (agentOffsetForWorld).  One 1024-thread
+// block per tile of 1024 worlds; tile sums come from K1's atomics (buffer
+// `parity`), the other parity's buffer is cleared for the next step.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(1024) void scan_kernel(SimState S)
+__device__ __forceinline__ int wave_incl_scan(int v)
 {
-    constexpr int T = 1024;
-    __shared__ int32_t sh[5][T];
-    __shared__ int32_t tot[5];
-    const int t = threadIdx.x;
-    const int W = (int)S.W;
-    const int per = (W + T - 1) / T;
-    const int w0 = t * per, w1 = min(W, w0 + per);
-    int32_t loc[5] = {0, 0, 0, 0, 0};
-    for (int w = w0; w < w1; ++w) {
-        const int4 c = reinterpret_cast<const int4 *>(S.scount)[w];
-        loc[0] += c.x; loc[1] += c.y; loc[2] += c.z; loc[3] += c.w;
-        loc[4] += S.n[w];
+    const int lane = (int)__lane_id();
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const int y = __shfl_up(v, d);
+        if (lane >= d) v += y;
     }
-    for (int k = 0; k < 5; ++k) sh[k][t] = loc[k];
-    __syncthreads();
-    // Hillis-Steele inclusive scan over the 1024 partial sums
-    for (int off = 1; off < T; off <<= 1) {
-        int32_t v[5];
-        for (int k = 0; k < 5; ++k) v[k] = (t >= off) ? sh[k][t - off] : 0;
-        __syncthreads();
-        for (int k = 0; k < 5; ++k) sh[k][t] += v[k];
-        __syncthreads();
+    return v;
+}
+
+__global__ __launch_bounds__(1024) void scan_kernel(SimState S, int parity)
+{
+    __shared__ int32_t s_pre[5], s_tot[5];
+    __shared__ int32_t s_wave[16][5];
+    const int t = threadIdx.x, b = blockIdx.x;
+    const int wv = t >> 6, lane = t & 63;
+    const int32_t *tiles = S.tiles + (size_t)parity * S.ntiles * 5;
+    if (t < 5) {
+        int32_t pre = 0, tot = 0;
+        for (uint32_t tt = 0; tt < S.ntiles; ++tt) {
+            const int32_t v = tiles[tt * 5 + t];
+            if ((int)tt < b) pre += v;
+            tot += v;
+        }
+        s_pre[t] = pre;
+        s_tot[t] = tot;
     }
-    if (t == T - 1) for (int k = 0; k < 5; ++k) tot[k] = sh[k][t];
+    const uint32_t w = (uint32_t)b * kTileWorlds + (uint32_t)t;
+    int32_t c[5] = {0, 0, 0, 0, 0};
+    if (w < S.W) {
+        const int4 sc = reinterpret_cast<const int4 *>(S.scount)[w];
+        c[0] = sc.x; c[1] = sc.y; c[2] = sc.z; c[3] = sc.w;
+        c[4] = sc.x + sc.y + sc.z + sc.w;
+    }
+    int32_t inc[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) inc[k] = wave_incl_scan(c[k]);
+    if (lane == 63) {
+#pragma unroll
+        for (int k = 0; k < 5; ++k) s_wave[wv][k] = inc[k];
+    }
     __syncthreads();
-    int32_t run[5];
-    for (int k = 0; k < 5; ++k) run[k] = sh[k][t] - loc[k];
-    const int32_t sb0 = 0, sb1 = tot[0], sb2 = tot[0] + tot[1], sb3 = tot[0] + tot[1] + tot[2];
-    for (int w = w0; w < w1; ++w) {
-        const int4 c = reinterpret_cast<const int4 *>(S.scount)[w];
+    if (t < 5) {
+        int32_t run = 0;
+        for (int i = 0; i < 16; ++i) { const int32_t v = s_wave[i][t]; s_wave[i][t] = run; run += v; }
+    }
+    __syncthreads();
+    if (w < S.W) {
+        int32_t ex[5];
+#pragma unroll
+        for (int k = 0; k < 5; ++k) ex[k] = s_pre[k] + s_wave[wv][k] + inc[k] - c[k];
         int4 rb;
-        rb.x = sb0 + run[0]; rb.y = sb1 + run[1]; rb.z = sb2 + run[2]; rb.w = sb3 + run[3];
+        rb.x = ex[0];
+        rb.y = s_tot[0] + ex[1];
+        rb.z = s_tot[0] + s_tot[1] + ex[2];
+        rb.w = s_tot[0] + s_tot[1] + s_tot[2] + ex[3];
         reinterpret_cast<int4 *>(S.row_base)[w] = rb;
-        S.world_off[w] = run[4];
-        run[0] += c.x; run[1] += c.y; run[2] += c.z; run[3] += c.w;
-        run[4] += S.n[w];
+        S.world_off[w] = ex[4];
     }
-    if (t == 0) {
-        S.totals[0] = (uint32_t)tot[4];
-        for (int k = 0; k < 4; ++k) S.totals[1 + k] = (uint32_t)tot[k];
-        *S.agent_steps += (unsigned long long)tot[4];
+    if (t < 5) S.tiles[(size_t)(parity ^ 1) * S.ntiles * 5 + b * 5 + t] = 0;
+    if (b == 0 && t == 0) {
+        S.totals[0] = (uint32_t)s_tot[4];
+        for (int k = 0; k < 4; ++k) S.totals[1 + k] = (uint32_t)s_tot[k];
+        *S.agent_steps += (unsigned long long)s_tot[4];
     }
 }
 
-// ---------------------------------------------------------------------------
-// K3: export -- updateObservations (sim.cpp:687-717), the species-major row
-// move, updateSensorOutputIdx (:736-789) and rewardSystem setting 8
-// (:840-983).  One wave per world writes its agents' rows into `nxt`,
-// carrying Action/HiddenState/Prev* from the old row in `cur`.
-// ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void export_kernel(SimState S, ObsTable cur, ObsTable nxt,
-                                                     int init)
+// init-only: tile sums straight from scount (no K1 ran yet)
+__global__ __launch_bounds__(1024) void tile_sum_kernel(SimState S, int parity)
 {
-    const uint32_t wv = threadIdx.x >> 6;
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t w = blockIdx.x * kWorldsPerBlock + wv;
-    if (w >= S.W) return;
-    const size_t base = (size_t)w * S.cap;
-    const int n = S.n[w];
-    const int4 rb = reinterpret_cast<const int4 *>(S.row_base)[w];
-    const float4 rew = reinterpret_cast<const float4 *>(S.sreward)[w];
-    const bool fixed = (S.flags & kFlagRewardFixed) != 0;
-    const bool depth = (S.flags & kFlagFixDepth) != 0;
-    // faithful B.3: rewards[4] reads the next SpeciesInfo row's rewards[0]
-    const float next_r0 = (w + 1 < S.W) ? S.sreward[(size_t)(w + 1) * kNumSpecies] : 0.0f;
-    int carry0 = 0, carry1 = 0, carry2 = 0, carry3 = 0;
-    for (int b = 0; b < n; b += 64) {
-        const int i = b + (int)lane;
-        const bool active = i < n;
-        const int32_t sp = active ? S.species[base + i] : 0;
-        const uint64_t m1 = ballot64(sp == 1), m2 = ballot64(sp == 2);
-        const uint64_t m3 = ballot64(sp == 3), m4 = ballot64(sp == 4);
-        int32_t row = 0;
-        if (sp == 1) row = rb.x + carry0 + (int32_t)rank_below(m1);
-        else if (sp == 2) row = rb.y + carry1 + (int32_t)rank_below(m2);
-        else if (sp == 3) row = rb.z + carry2 + (int32_t)rank_below(m3);
-        else if (sp == 4) row = rb.w + carry3 + (int32_t)rank_below(m4);
-        carry0 += __popcll(m1); carry1 += __popcll(m2);
-        carry2 += __popcll(m3); carry3 += __popcll(m4);
-        if (!active) continue;
-
-        const size_t r = (size_t)row;
-        const float x = S.x[base + i], y = S.y[base + i];
-        const int32_t h = S.health[base + i];
-        const float s0 = init ? 0.0f : S.sur0[base + i];
-        const float s1 = init ? 0.0f : S.sur1[base + i];
-        const uint32_t st = init ? 0u : S.stats[base + i];
-        const int32_t orow = S.obsrow[base + i];
-
-        nxt.species[r] = sp;
-        reinterpret_cast<float2 *>(nxt.pos)[r] = make_float2(x, y);
-        nxt.health[r] = h;
-        reinterpret_cast<float2 *>(nxt.sur)[r] = make_float2(s0, s1);
-        const int4 stv = make_int4((int)(st & 1u), (int)((st >> 1) & 1u), (int)((st >> 2) & 1u),
-                                   (int)((st >> 3) & 1u));
-        reinterpret_cast<int4 *>(nxt.stats)[r] = stv;
-
-        // rewardSystem, setting 8 (sim.cpp:942-956)
-        float rv = 0.0f;
-        if (!init) {
-            float sr;
-            if (fixed) sr = sp == 1 ? rew.x : sp == 2 ? rew.y : sp == 3 ? rew.z : rew.w;
-            else sr = sp == 1 ? rew.y : sp == 2 ? rew.z : sp == 3 ? rew.w : next_r0;
-            rv = sr + (float)h / 100.0f - 0.5f;
-            if (stv.z) rv += 10.0f;
-            if (stv.w) rv += 10.0f;
-            if (stv.y) rv += 15.0f;
-        }
-        nxt.reward[r] = rv;
-
-        int2 a0 = make_int2(0, 0), a1 = a0, a2 = a0, pa0 = a0, pa1 = a0, pa2 = a0;
-        float4 h0 = make_float4(0.f, 0.f, 0.f, 0.f), h1 = h0, h2 = h0, h3 = h0;
-        float4 q0 = h0, q1 = h0, q2 = h0, q3 = h0;
-        int32_t psp = 0, ph = 0;
-        float2 ppos = make_float2(0.f, 0.f), psur = ppos;
-        float prew = 0.0f;
-        int4 pst = make_int4(0, 0, 0, 0);
-        uint4 sem0 = make_uint4(0u, 0u, 0u, 0u), sem1 = sem0, dep0 = sem0, dep1 = sem0;
-        if (orow >= 0) {
-            const size_t o = (size_t)orow;
-            const int2 *ap = reinterpret_cast<const int2 *>(cur.action + o * 6);
-            a0 = ap[0]; a1 = ap[1]; a2 = ap[2];
-            const float4 *hp = reinterpret_cast<const float4 *>(cur.hidden + o * kHidden);
-            h0 = hp[0]; h1 = hp[1]; h2 = hp[2]; h3 = hp[3];
-            psp = cur.pspecies[o];
-            ppos = reinterpret_cast<const float2 *>(cur.ppos)[o];
-            ph = cur.phealth[o];
-            psur = reinterpret_cast<const float2 *>(cur.psur)[o];
-            prew = cur.preward[o];
-            const int2 *pap = reinterpret_cast<const int2 *>(cur.paction + o * 6);
-            pa0 = pap[0]; pa1 = pap[1]; pa2 = pap[2];
-            pst = reinterpret_cast<const int4 *>(cur.pstats)[o];
-            const float4 *php = reinterpret_cast<const float4 *>(cur.phidden + o * kHidden);
-            q0 = php[0]; q1 = php[1]; q2 = php[2]; q3 = php[3];
-            const uint4 *sp4 = reinterpret_cast<const uint4 *>(cur.sem + o * kSensor);
-            sem0 = sp4[0]; sem1 = sp4[1];
-            if (depth) {
-                const uint4 *dp4 = reinterpret_cast<const uint4 *>(cur.depth + o * kSensor);
-                dep0 = dp4[0]; dep1 = dp4[1];
-            }
-        }
-        int2 *nap = reinterpret_cast<int2 *>(nxt.action + r * 6);
-        nap[0] = a0; nap[1] = a1; nap[2] = a2;
-        float4 *nhp = reinterpret_cast<float4 *>(nxt.hidden + r * kHidden);
-        nhp[0] = h0; nhp[1] = h1; nhp[2] = h2; nhp[3] = h3;
-        nxt.pspecies[r] = psp;
-        reinterpret_cast<float2 *>(nxt.ppos)[r] = ppos;
-        nxt.phealth[r] = ph;
-        reinterpret_cast<float2 *>(nxt.psur)[r] = psur;
-        nxt.preward[r] = prew;
-        int2 *npap = reinterpret_cast<int2 *>(nxt.paction + r * 6);
-        npap[0] = pa0; npap[1] = pa1; npap[2] = pa2;
-        reinterpret_cast<int4 *>(nxt.pstats)[r] = pst;
-        float4 *nphp = reinterpret_cast<float4 *>(nxt.phidden + r * kHidden);
-        nphp[0] = q0; nphp[1] = q1; nphp[2] = q2; nphp[3] = q3;
-        uint4 *nps = reinterpret_cast<uint4 *>(nxt.psem + r * kSensor);
-        nps[0] = sem0; nps[1] = sem1;
-        if (depth) {
-            uint4 *npd = reinterpret_cast<uint4 *>(nxt.pdepth + r * kSensor);
-            npd[0] = dep0; npd[1] = dep1;
-        }
-        S.obsrow[base + i] = row;
+    __shared__ int32_t s_wave[16][5];
+    const int t = threadIdx.x, b = blockIdx.x;
+    const uint32_t w = (uint32_t)b * kTileWorlds + (uint32_t)t;
+    int32_t c[5] = {0, 0, 0, 0, 0};
+    if (w < S.W) {
+        const int4 sc = reinterpret_cast<const int4 *>(S.scount)[w];
+        c[0] = sc.x; c[1] = sc.y; c[2] = sc.z; c[3] = sc.w;
+        c[4] = sc.x + sc.y + sc.z + sc.w;
+    }
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+        const int32_t v = wave_incl_scan(c[k]);
+        if ((t & 63) == 63) s_wave[t >> 6][k] = v;
+    }
+    __syncthreads();
+    if (t < 5) {
+        int32_t run = 0;
+        for (int i = 0; i < 16; ++i) run += s_wave[i][t];
+        S.tiles[(size_t)parity * S.ntiles * 5 + b * 5 + t] = run;
+        S.tiles[(size_t)(parity ^ 1) * S.ntiles * 5 + b * 5 + t] = 0;
     }
 }
 
+constexpr int kMaxFood = kFoodCap + 2;        // live packages == currentNumFood <= 30
 // ---------------------------------------------------------------------------
-// K4: sensor -- 32-pixel raycast (24 forward + 8 backward) plus the finder ray
+// K3 sensor part -- 32-pixel raycast (24 forward + 8 backward) plus the finder ray
 // (Madrona RenderingSystem, sim.cpp:1183-1188).  Build spec:
 // objects are unit circles; in an agent's frame (f along heading h, l along
 // r = (hy, -hx)) ray h + u r meets a circle iff
@@ -536,7 +518,6 @@ __global__ __launch_bounds__(256) void export_kernel(SimState S, ObsTable cur, O
 // ---------------------------------------------------------------------------
 constexpr int kKeyAgents = 8;                 // agents per chunk (key rows)
 constexpr int kQueue = 128;                   // survivor queue entries
-constexpr int kMaxFood = kFoodCap + 2;        // live packages == currentNumFood <= 30
 constexpr float kWedge = 1.41421356f + 0.05f; // |l| <= |f| + sqrt(2) (+ margin)
 constexpr float kUEps = 2e-3f;                // root-interval margin in u
 constexpr uint32_t kOrderFood = 1u;           // object order: wall 0, food 1.., agents 64..
@@ -547,6 +528,7 @@ struct SensorLDS {
     float ox[kMaxFood + kMaxCap], oy[kMaxFood + kMaxCap];   // food then agents
     float hx[kMaxCap], hy[kMaxCap];
     int32_t sp[kMaxCap];
+    int32_t row[kMaxCap];                                   // new export row per slot
     unsigned long long key[kKeyAgents * kRays];
     uint32_t queue[kQueue];
     float u[kSensor];
@@ -700,7 +682,19 @@ __device__ __forceinline__ void process_queue(SensorLDS &L, int a0, int nf, int 
     }
 }
 
-__global__ __launch_bounds__(256) void sensor_kernel(SimState S, ObsTable nxt)
+
+// ---------------------------------------------------------------------------
+// K3: export + sensor, one wave per world.
+//  * updateObservations (sim.cpp:687-717) into the world's species-major rows
+//    of the next table, carrying Action / HiddenState / Prev* from the old row
+//    (the obs row travels through the species sort), updateSensorOutputIdx's
+//    prev-sensor copy (sim.cpp:736-789), rewardSystem setting 8
+//    (sim.cpp:840-983, faithful rewards[speciesID] off-by-one unless fixed);
+//  * then the raycast sensor (Sensor graph, sim.cpp:1183-1188) into the new
+//    rows, and the finder slot for the next step's shoot / breed.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void export_sensor_kernel(SimState S, ObsTable cur,
+                                                            ObsTable nxt, int init)
 {
     __shared__ SensorLDS lds[kWorldsPerBlock];
     const uint32_t wv = threadIdx.x >> 6;
@@ -713,37 +707,149 @@ __global__ __launch_bounds__(256) void sensor_kernel(SimState S, ObsTable nxt)
     const bool depth = (S.flags & kFlagFixDepth) != 0;
     if (lane < kSensor) L.u[lane] = kURay[lane];
 
-    // live food packages in (chunk, package) order -> objects [0, nf)
-    int nf = 0;
-    for (int b = 0; b < kNumPkg; b += 64) {
-        const int k = b + (int)lane;
-        const uint32_t p = k < kNumPkg ? S.food[(size_t)w * kNumPkg + k] : 0u;
-        const bool live = (p >> 16) != 0u;
-        const uint64_t m = ballot64(live);
-        if (live) {
-            const int c = k / kMaxPkg;
-            const int s = nf + (int)rank_below(m);
-            if (s < kMaxFood) {   // live packages == currentNumFood <= 30 (addFoodSystem)
-                L.ox[s] = (float)(p & 0xFFu) + (float)((c % kChunksX) * kChunkW);
-                L.oy[s] = (float)((p >> 8) & 0xFFu) + (float)((c / kChunksX) * kChunkW);
+    // ---- live food packages in (chunk, package) order -> objects [0, nf) ----
+    int nf;
+    {
+        uint64_t rec = 0;
+        if (lane < kNumChunks) rec = S.food[(size_t)w * kNumChunks + lane];
+        const uint32_t live = (uint32_t)(rec >> 40) & 31u;
+        const int cnt = __popc(live);
+        int off = 0, tot = 0;
+#pragma unroll
+        for (int bt = 0; bt < 3; ++bt) {
+            const uint64_t m = ballot64((cnt >> bt) & 1);
+            off += (int)rank_below(m) << bt;
+            tot += __popcll(m) << bt;
+        }
+        const float bx = (float)((lane % kChunksX) * kChunkW);
+        const float by = (float)((lane / kChunksX) * kChunkW);
+        int s = off;
+#pragma unroll
+        for (int k = 0; k < kMaxPkg; ++k) {
+            if ((live >> k) & 1u) {
+                const uint32_t xy = (uint32_t)(rec >> (8 * k)) & 0xFFu;
+                if (s < kMaxFood) {   // live packages == currentNumFood <= 30
+                    L.ox[s] = (float)(xy & 15u) + bx;
+                    L.oy[s] = (float)(xy >> 4) + by;
+                }
+                ++s;
             }
         }
-        nf += __popcll(m);
+        nf = min(tot, kMaxFood);
     }
-    nf = min(nf, kMaxFood);
-    // agents -> objects [nf, nf + n)
-    for (int i = lane; i < n; i += 64) {
-        L.ox[nf + i] = S.x[base + i];
-        L.oy[nf + i] = S.y[base + i];
-        L.sp[i] = S.species[base + i];
-        float dx, dy;
-        heading(S.rw[base + i], S.rz[base + i], dx, dy);
-        L.hx[i] = dx;
-        L.hy[i] = dy;
+
+    // ---- export rows ----
+    const int4 rb = reinterpret_cast<const int4 *>(S.row_base)[w];
+    const float4 rew = reinterpret_cast<const float4 *>(S.sreward)[w];
+    const bool fixed = (S.flags & kFlagRewardFixed) != 0;
+    // faithful B.3: rewards[4] reads the next SpeciesInfo row's rewards[0]
+    const float next_r0 = (w + 1 < S.W) ? S.sreward[(size_t)(w + 1) * kNumSpecies] : 0.0f;
+    int carry0 = 0, carry1 = 0, carry2 = 0, carry3 = 0;
+    for (int b = 0; b < n; b += 64) {
+        const int i = b + (int)lane;
+        const bool active = i < n;
+        const int32_t sp = active ? S.species[base + i] : 0;
+        const uint64_t m1 = ballot64(sp == 1), m2 = ballot64(sp == 2);
+        const uint64_t m3 = ballot64(sp == 3), m4 = ballot64(sp == 4);
+        int32_t row = 0;
+        if (sp == 1) row = rb.x + carry0 + (int32_t)rank_below(m1);
+        else if (sp == 2) row = rb.y + carry1 + (int32_t)rank_below(m2);
+        else if (sp == 3) row = rb.z + carry2 + (int32_t)rank_below(m3);
+        else if (sp == 4) row = rb.w + carry3 + (int32_t)rank_below(m4);
+        carry0 += __popcll(m1); carry1 += __popcll(m2);
+        carry2 += __popcll(m3); carry3 += __popcll(m4);
+        if (!active) continue;
+
+        const size_t r = (size_t)row;
+        const float x = S.x[base + i], y = S.y[base + i];
+        const int32_t h = S.health[base + i];
+        const float s0 = init ? 0.0f : S.sur0[base + i];
+        const float s1 = init ? 0.0f : S.sur1[base + i];
+        const uint32_t st = init ? 0u : S.stats[base + i];
+        const int32_t orow = S.obsrow[base + i];
+        {
+            float hx, hy;
+            heading(S.rw[base + i], S.rz[base + i], hx, hy);
+            L.ox[nf + i] = x;
+            L.oy[nf + i] = y;
+            L.sp[i] = sp;
+            L.hx[i] = hx;
+            L.hy[i] = hy;
+            L.row[i] = row;
+        }
+
+        nxt.species[r] = sp;
+        reinterpret_cast<float2 *>(nxt.pos)[r] = make_float2(x, y);
+        nxt.health[r] = h;
+        reinterpret_cast<float2 *>(nxt.sur)[r] = make_float2(s0, s1);
+        const int4 stv = make_int4((int)(st & 1u), (int)((st >> 1) & 1u), (int)((st >> 2) & 1u),
+                                   (int)((st >> 3) & 1u));
+        reinterpret_cast<int4 *>(nxt.stats)[r] = stv;
+        float rv = 0.0f;
+        if (!init) {
+            float sr;
+            if (fixed) sr = sp == 1 ? rew.x : sp == 2 ? rew.y : sp == 3 ? rew.z : rew.w;
+            else sr = sp == 1 ? rew.y : sp == 2 ? rew.z : sp == 3 ? rew.w : next_r0;
+            rv = sr + (float)h / 100.0f - 0.5f;
+            if (stv.z) rv += 10.0f;
+            if (stv.w) rv += 10.0f;
+            if (stv.y) rv += 15.0f;
+        }
+        nxt.reward[r] = rv;
+        S.obsrow[base + i] = row;
+
+        int2 *nap = reinterpret_cast<int2 *>(nxt.action + r * 6);
+        float4 *nhp = reinterpret_cast<float4 *>(nxt.hidden + r * kHidden);
+        int2 *npap = reinterpret_cast<int2 *>(nxt.paction + r * 6);
+        float4 *nphp = reinterpret_cast<float4 *>(nxt.phidden + r * kHidden);
+        uint4 *nps = reinterpret_cast<uint4 *>(nxt.psem + r * kSensor);
+        if (orow >= 0) {
+            const size_t o = (size_t)orow;
+            const int2 *ap = reinterpret_cast<const int2 *>(cur.action + o * 6);
+            nap[0] = ap[0]; nap[1] = ap[1]; nap[2] = ap[2];
+            const float4 *hp = reinterpret_cast<const float4 *>(cur.hidden + o * kHidden);
+            nhp[0] = hp[0]; nhp[1] = hp[1]; nhp[2] = hp[2]; nhp[3] = hp[3];
+            nxt.pspecies[r] = cur.pspecies[o];
+            reinterpret_cast<float2 *>(nxt.ppos)[r] = reinterpret_cast<const float2 *>(cur.ppos)[o];
+            nxt.phealth[r] = cur.phealth[o];
+            reinterpret_cast<float2 *>(nxt.psur)[r] = reinterpret_cast<const float2 *>(cur.psur)[o];
+            nxt.preward[r] = cur.preward[o];
+            const int2 *pap = reinterpret_cast<const int2 *>(cur.paction + o * 6);
+            npap[0] = pap[0]; npap[1] = pap[1]; npap[2] = pap[2];
+            reinterpret_cast<int4 *>(nxt.pstats)[r] = reinterpret_cast<const int4 *>(cur.pstats)[o];
+            const float4 *php = reinterpret_cast<const float4 *>(cur.phidden + o * kHidden);
+            nphp[0] = php[0]; nphp[1] = php[1]; nphp[2] = php[2]; nphp[3] = php[3];
+            const uint4 *sp4 = reinterpret_cast<const uint4 *>(cur.sem + o * kSensor);
+            nps[0] = sp4[0]; nps[1] = sp4[1];
+            if (depth) {
+                const uint4 *dp4 = reinterpret_cast<const uint4 *>(cur.depth + o * kSensor);
+                uint4 *npd = reinterpret_cast<uint4 *>(nxt.pdepth + r * kSensor);
+                npd[0] = dp4[0]; npd[1] = dp4[1];
+            }
+        } else {
+            const int2 z2 = make_int2(0, 0);
+            const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
+            const uint4 zu = make_uint4(0u, 0u, 0u, 0u);
+            nap[0] = z2; nap[1] = z2; nap[2] = z2;
+            nhp[0] = z4; nhp[1] = z4; nhp[2] = z4; nhp[3] = z4;
+            nxt.pspecies[r] = 0;
+            reinterpret_cast<float2 *>(nxt.ppos)[r] = make_float2(0.f, 0.f);
+            nxt.phealth[r] = 0;
+            reinterpret_cast<float2 *>(nxt.psur)[r] = make_float2(0.f, 0.f);
+            nxt.preward[r] = 0.0f;
+            npap[0] = z2; npap[1] = z2; npap[2] = z2;
+            reinterpret_cast<int4 *>(nxt.pstats)[r] = make_int4(0, 0, 0, 0);
+            nphp[0] = z4; nphp[1] = z4; nphp[2] = z4; nphp[3] = z4;
+            nps[0] = zu; nps[1] = zu;
+            if (depth) {
+                uint4 *npd = reinterpret_cast<uint4 *>(nxt.pdepth + r * kSensor);
+                npd[0] = zu; npd[1] = zu;
+            }
+        }
     }
+    if (init) return;
     const int nobj = nf + n;
     wave_sync();
-
     for (int a0 = 0; a0 < n; a0 += kKeyAgents) {
         const int nc = min(kKeyAgents, n - a0);
         for (int q = lane; q < nc * kRays; q += 64) L.key[q] = kNoHit;
@@ -801,7 +907,7 @@ __global__ __launch_bounds__(256) void sensor_kernel(SimState S, ObsTable nxt)
             depv |= __shfl_xor(depv, 1);
             depv |= __shfl_xor(depv, 2);
             if (valid && (lane & 3u) == 0u) {
-                const size_t r = (size_t)S.obsrow[base + a0 + ci];
+                const size_t r = (size_t)L.row[a0 + ci];
                 reinterpret_cast<uint32_t *>(nxt.sem + r * kSensor)[px >> 2] = semv;
                 if (depth) reinterpret_cast<uint32_t *>(nxt.depth + r * kSensor)[px >> 2] = depv;
             }
@@ -820,29 +926,36 @@ __global__ __launch_bounds__(256) void sensor_kernel(SimState S, ObsTable nxt)
 }
 
 // ---------------------------------------------------------------------------
-// shiftObservationsSystem + shiftHiddenState (sim.cpp:1002-1048): Prev* <-
-// current for rows [0, N), with the reference's prevStats.hitEnemyAgent =
-// stats.hitFriendlyAgent (sim.cpp:1034).  N is read on the device.
+// K5: shiftObservationsSystem + shiftHiddenState (sim.cpp:1002-1048): Prev* <-
+// current for rows [0, N).  Each column is a contiguous byte range, so the copy
+// is one grid-stride stream of 16-byte granules over the concatenation of the
+// 8 columns (N is read on the device; granules past a column's end land in its
+// 256-B allocation padding / unused capacity rows).  PrevStats rows get the
+// reference's prevStats.hitEnemyAgent = stats.hitFriendlyAgent (sim.cpp:1034).
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void shift_kernel(const uint32_t *totals, ObsTable t)
 {
     const uint32_t N = totals[0];
+    const uint32_t g4 = (4u * N + 15u) >> 4, g8 = (8u * N + 15u) >> 4, g24 = (24u * N + 15u) >> 4;
+    // segment ends (in granules): species, pos, health, sur, reward, action, stats, hidden
+    const uint32_t e0 = g4, e1 = e0 + g8, e2 = e1 + g4, e3 = e2 + g8, e4 = e3 + g4,
+                   e5 = e4 + g24, e6 = e5 + N, e7 = e6 + 4u * N;
     const uint32_t stride = gridDim.x * blockDim.x;
-    for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r < N; r += stride) {
-        t.pspecies[r] = t.species[r];
-        reinterpret_cast<float2 *>(t.ppos)[r] = reinterpret_cast<const float2 *>(t.pos)[r];
-        t.phealth[r] = t.health[r];
-        reinterpret_cast<float2 *>(t.psur)[r] = reinterpret_cast<const float2 *>(t.sur)[r];
-        t.preward[r] = t.reward[r];
-        const int2 *a = reinterpret_cast<const int2 *>(t.action + (size_t)r * 6);
-        int2 *pa = reinterpret_cast<int2 *>(t.paction + (size_t)r * 6);
-        pa[0] = a[0]; pa[1] = a[1]; pa[2] = a[2];
-        int4 s = reinterpret_cast<const int4 *>(t.stats)[r];
-        s.y = s.x;
-        reinterpret_cast<int4 *>(t.pstats)[r] = s;
-        const float4 *h = reinterpret_cast<const float4 *>(t.hidden + (size_t)r * kHidden);
-        float4 *ph = reinterpret_cast<float4 *>(t.phidden + (size_t)r * kHidden);
-        ph[0] = h[0]; ph[1] = h[1]; ph[2] = h[2]; ph[3] = h[3];
+    for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g < e7; g += stride) {
+        const uint4 *src;
+        uint4 *dst;
+        uint32_t k;
+        if (g < e0) { src = (const uint4 *)t.species; dst = (uint4 *)t.pspecies; k = g; }
+        else if (g < e1) { src = (const uint4 *)t.pos; dst = (uint4 *)t.ppos; k = g - e0; }
+        else if (g < e2) { src = (const uint4 *)t.health; dst = (uint4 *)t.phealth; k = g - e1; }
+        else if (g < e3) { src = (const uint4 *)t.sur; dst = (uint4 *)t.psur; k = g - e2; }
+        else if (g < e4) { src = (const uint4 *)t.reward; dst = (uint4 *)t.preward; k = g - e3; }
+        else if (g < e5) { src = (const uint4 *)t.action; dst = (uint4 *)t.paction; k = g - e4; }
+        else if (g < e6) { src = (const uint4 *)t.stats; dst = (uint4 *)t.pstats; k = g - e5; }
+        else { src = (const uint4 *)t.hidden; dst = (uint4 *)t.phidden; k = g - e6; }
+        uint4 v = src[k];
+        if (g >= e5 && g < e6) v.y = v.x;
+        dst[k] = v;
     }
 }
 
@@ -875,7 +988,7 @@ __global__ __launch_bounds__(256) void init_kernel(SimState S)
         S.sur1[base + i] = 0.0f;
         S.stats[base + i] = 0u;
     }
-    for (int k = lane; k < kNumPkg; k += 64) S.food[(size_t)w * kNumPkg + k] = 0u;
+    if (lane < kNumChunks) S.food[(size_t)w * kNumChunks + lane] = 0ull;
     if (lane < kNumSpecies) {
         S.scount[(size_t)w * kNumSpecies + lane] = A / kNumSpecies + ((int)lane < A % kNumSpecies ? 1 : 0);
         S.sreward[(size_t)w * kNumSpecies + lane] = 0.0f;
@@ -937,39 +1050,38 @@ __global__ __launch_bounds__(256) void sensor_index_kernel(SimState S, int32_t *
 // ---------------------------------------------------------------------------
 static inline unsigned world_blocks(uint32_t W) { return (W + kWorldsPerBlock - 1) / kWorldsPerBlock; }
 
+uint32_t scan_tiles(uint32_t W) { return (W + kTileWorlds - 1) / kTileWorlds; }
+
 hipError_t launch_init(const SimState &S, hipStream_t st)
 {
     hipLaunchKernelGGL(init_kernel, dim3(world_blocks(S.W)), dim3(256), 0, st, S);
     return hipGetLastError();
 }
-hipError_t launch_world_step(const SimState &S, const ObsTable &cur, hipStream_t st)
+hipError_t launch_tile_sum(const SimState &S, int parity, hipStream_t st)
 {
-    hipLaunchKernelGGL(world_step_kernel, dim3(world_blocks(S.W)), dim3(256), 0, st, S, cur);
+    hipLaunchKernelGGL(tile_sum_kernel, dim3(S.ntiles), dim3(1024), 0, st, S, parity);
     return hipGetLastError();
 }
-hipError_t launch_scan(const SimState &S, hipStream_t st)
+hipError_t launch_world_step(const SimState &S, const ObsTable &cur, int parity, hipStream_t st)
 {
-    hipLaunchKernelGGL(scan_kernel, dim3(1), dim3(1024), 0, st, S);
+    hipLaunchKernelGGL(world_step_kernel, dim3(world_blocks(S.W)), dim3(256), 0, st, S, cur, parity);
     return hipGetLastError();
 }
-hipError_t launch_export(const SimState &S, const ObsTable &cur, const ObsTable &nxt, int init,
-                         hipStream_t st)
+hipError_t launch_scan(const SimState &S, int parity, hipStream_t st)
 {
-    hipLaunchKernelGGL(export_kernel, dim3(world_blocks(S.W)), dim3(256), 0, st, S, cur, nxt, init);
+    hipLaunchKernelGGL(scan_kernel, dim3(S.ntiles), dim3(1024), 0, st, S, parity);
     return hipGetLastError();
 }
-hipError_t launch_sensor(const SimState &S, const ObsTable &nxt, hipStream_t st)
+hipError_t launch_export_sensor(const SimState &S, const ObsTable &cur, const ObsTable &nxt,
+                                int init, hipStream_t st)
 {
-    hipLaunchKernelGGL(sensor_kernel, dim3(world_blocks(S.W)), dim3(256), 0, st, S, nxt);
+    hipLaunchKernelGGL(export_sensor_kernel, dim3(world_blocks(S.W)), dim3(256), 0, st, S, cur,
+                       nxt, init);
     return hipGetLastError();
 }
 hipError_t launch_shift(const SimState &S, const ObsTable &t, hipStream_t st)
 {
-    unsigned rows = S.W * S.cap;
-    unsigned blocks = (rows + 255) / 256;
-    if (blocks > 4096) blocks = 4096;
-    if (blocks == 0) blocks = 1;
-    hipLaunchKernelGGL(shift_kernel, dim3(blocks), dim3(256), 0, st, S.totals, t);
+    hipLaunchKernelGGL(shift_kernel, dim3(4096), dim3(256), 0, st, S.totals, t);
     return hipGetLastError();
 }
 hipError_t launch_synthetic_actions(const SimState &S, const ObsTable &t, uint32_t seed,

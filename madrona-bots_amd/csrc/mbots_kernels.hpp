@@ -20,7 +20,7 @@ struct SimState {
     int32_t *n;                     // [W] live agents per world
     uint32_t *ctr;                  // [W] RNG counter
     uint2 *key;                     // [W] RNG key
-    uint32_t *food;                 // [W][240] packed x | y << 8 | numFood << 16
+    uint64_t *food;                 // [W][48] per chunk: 5 x (x | y << 4) bytes, live mask << 40
     int32_t *cur_food;              // [W] Sim::currentNumFood
     float *sreward;                 // [W][4] SpeciesReward
     int32_t *scount;                // [W][4] SpeciesCount (exported)
@@ -28,8 +28,9 @@ struct SimState {
     int32_t *world_off;             // [W] world-major agent offsets
     uint32_t *overflow;             // [W] dropped births/respawns
     uint32_t *totals;               // [0] = N, [1..4] = per-species rows
+    int32_t *tiles;                 // [2][ntiles][5] per-tile species/agent counts (K1 -> K2)
     unsigned long long *agent_steps;
-    uint32_t W, cap, A, world_offset, flags, seed;
+    uint32_t W, cap, A, world_offset, flags, seed, ntiles;
 };
 
 // One half of the double-buffered species-major observation table
@@ -41,12 +42,13 @@ struct ObsTable {
     int32_t *paction;  int32_t *pstats; float *phidden; int8_t *psem; uint8_t *pdepth;
 };
 
+uint32_t scan_tiles(uint32_t W);
 hipError_t launch_init(const SimState &S, hipStream_t st);
-hipError_t launch_world_step(const SimState &S, const ObsTable &cur, hipStream_t st);
-hipError_t launch_scan(const SimState &S, hipStream_t st);
-hipError_t launch_export(const SimState &S, const ObsTable &cur, const ObsTable &nxt, int init,
-                         hipStream_t st);
-hipError_t launch_sensor(const SimState &S, const ObsTable &nxt, hipStream_t st);
+hipError_t launch_tile_sum(const SimState &S, int parity, hipStream_t st);
+hipError_t launch_world_step(const SimState &S, const ObsTable &cur, int parity, hipStream_t st);
+hipError_t launch_scan(const SimState &S, int parity, hipStream_t st);
+hipError_t launch_export_sensor(const SimState &S, const ObsTable &cur, const ObsTable &nxt,
+                                int init, hipStream_t st);
 hipError_t launch_shift(const SimState &S, const ObsTable &t, hipStream_t st);
 hipError_t launch_synthetic_actions(const SimState &S, const ObsTable &t, uint32_t seed,
                                     uint32_t step, int write_hidden, hipStream_t st);

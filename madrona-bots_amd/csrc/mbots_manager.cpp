@@ -64,6 +64,7 @@ struct mbots_handle {
     mbots::SimState S{};
     mbots::ObsTable T[2]{};
     int tb = 0;
+    int parity = 0;                   // K1 -> K2 tile-count buffer of this step
     Arena arena;
     int32_t *done_zeros = nullptr;    // Done column (never written, sim.cpp:74-75, B.7)
     int32_t *reset_zeros = nullptr;   // WorldReset singleton per world
@@ -153,7 +154,7 @@ size_t layout(mbots_handle *h, Arena &a)
     S.n = a.take<int32_t>(W);
     S.ctr = a.take<uint32_t>(W);
     S.key = a.take<uint2>(W);
-    S.food = a.take<uint32_t>(W * kNumPkg);
+    S.food = a.take<uint64_t>(W * kNumChunks);
     S.cur_food = a.take<int32_t>(W);
     S.sreward = a.take<float>(W * kNumSpecies);
     S.scount = a.take<int32_t>(W * kNumSpecies);
@@ -161,6 +162,8 @@ size_t layout(mbots_handle *h, Arena &a)
     S.world_off = a.take<int32_t>(W);
     S.overflow = a.take<uint32_t>(W);
     S.totals = a.take<uint32_t>(8);
+    S.ntiles = scan_tiles((uint32_t)W);
+    S.tiles = a.take<int32_t>((size_t)2 * S.ntiles * 5);
     S.agent_steps = a.take<unsigned long long>(1);
     fill_table(h->T[0], a, rows);
     fill_table(h->T[1], a, rows);
@@ -250,8 +253,9 @@ int mbots_create(const mbots_config *cfg_in, mbots_handle **out)
     check(hipMemsetAsync(h->arena.base, 0, bytes, st), "hipMemsetAsync");
     // Sim::Sim / initWorld (sim.cpp:1232-1256) + initial export of the rows
     check(mbots::launch_init(S, st), "init_kernel");
-    check(mbots::launch_scan(S, st), "scan_kernel");
-    check(mbots::launch_export(S, h->T[1], h->T[0], 1, st), "export_kernel(init)");
+    check(mbots::launch_tile_sum(S, 0, st), "tile_sum_kernel");
+    check(mbots::launch_scan(S, 0, st), "scan_kernel");
+    check(mbots::launch_export_sensor(S, h->T[1], h->T[0], 1, st), "export_sensor_kernel(init)");
     if (rc == MBOTS_OK) rc = record_totals(h, st);
     check(hipStreamSynchronize(st), "hipStreamSynchronize");
     if (rc != MBOTS_OK) {
@@ -262,6 +266,7 @@ int mbots_create(const mbots_config *cfg_in, mbots_handle **out)
     unsigned long long zero = 0;
     check(hipMemcpy(S.agent_steps, &zero, sizeof(zero), hipMemcpyHostToDevice), "hipMemcpy");
     h->tb = 0;
+    h->parity = 1;   // the init scan consumed buffer 0 and cleared buffer 1
     *out = h;
     return rc;
 }
@@ -289,13 +294,15 @@ int mbots_step(mbots_handle *h, void *stream)
     const mbots::ObsTable &cur = h->T[h->tb];
     const mbots::ObsTable &nxt = h->T[h->tb ^ 1];
     int rc;
-    if ((rc = timed(h, MBOTS_TK_WORLD_STEP, st, [&] { return mbots::launch_world_step(h->S, cur, st); })))
+    const int par = h->parity;
+    if ((rc = timed(h, MBOTS_TK_WORLD_STEP, st,
+                    [&] { return mbots::launch_world_step(h->S, cur, par, st); })))
         return rc;
-    if ((rc = timed(h, MBOTS_TK_SCAN, st, [&] { return mbots::launch_scan(h->S, st); }))) return rc;
-    if ((rc = timed(h, MBOTS_TK_EXPORT, st, [&] { return mbots::launch_export(h->S, cur, nxt, 0, st); })))
+    if ((rc = timed(h, MBOTS_TK_SCAN, st, [&] { return mbots::launch_scan(h->S, par, st); }))) return rc;
+    if ((rc = timed(h, MBOTS_TK_EXPORT, st,
+                    [&] { return mbots::launch_export_sensor(h->S, cur, nxt, 0, st); })))
         return rc;
-    if ((rc = timed(h, MBOTS_TK_SENSOR, st, [&] { return mbots::launch_sensor(h->S, nxt, st); })))
-        return rc;
+    h->parity ^= 1;
     h->tb ^= 1;
     return record_totals(h, st);
 }
