@@ -492,45 +492,164 @@ __global__ __launch_bounds__(1024) void tile_sum_kernel(SimState S, int parity)
     }
 }
 
-constexpr int kMaxFood = kFoodCap + 2;        // live packages == currentNumFood <= 30
 // ---------------------------------------------------------------------------
-// K3 sensor part -- 32-pixel raycast (24 forward + 8 backward) plus the finder ray
+// K3a: export rows, one wave per world -- updateObservations (sim.cpp:687-717)
+// into the world's species-major rows of the next table and rewardSystem
+// setting 8 (sim.cpp:840-983; faithful rewards[speciesID] off-by-one unless
+// fixed).  The old row of each agent (the obs row travels through the species
+// sort with its Action / HiddenState / Prev* columns and the prev sensor,
+// updateSensorOutputIdx sim.cpp:736-789) is recorded in src_of[new_row] for
+// the K4 move stream.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void export_rows_kernel(SimState S, ObsTable nxt, int init)
+{
+    const uint32_t wv = threadIdx.x >> 6;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t w = blockIdx.x * kWorldsPerBlock + wv;
+    if (w >= S.W) return;
+    const size_t base = (size_t)w * S.cap;
+    const int n = S.n[w];
+    const int4 rb = reinterpret_cast<const int4 *>(S.row_base)[w];
+    const float4 rew = reinterpret_cast<const float4 *>(S.sreward)[w];
+    const bool fixed = (S.flags & kFlagRewardFixed) != 0;
+    // faithful B.3: rewards[4] reads the next SpeciesInfo row's rewards[0]
+    const float next_r0 = (w + 1 < S.W) ? S.sreward[(size_t)(w + 1) * kNumSpecies] : 0.0f;
+    int carry0 = 0, carry1 = 0, carry2 = 0, carry3 = 0;
+    for (int b = 0; b < n; b += 64) {
+        const int i = b + (int)lane;
+        const bool active = i < n;
+        const int32_t sp = active ? S.species[base + i] : 0;
+        const uint64_t m1 = ballot64(sp == 1), m2 = ballot64(sp == 2);
+        const uint64_t m3 = ballot64(sp == 3), m4 = ballot64(sp == 4);
+        int32_t row = 0;
+        if (sp == 1) row = rb.x + carry0 + (int32_t)rank_below(m1);
+        else if (sp == 2) row = rb.y + carry1 + (int32_t)rank_below(m2);
+        else if (sp == 3) row = rb.z + carry2 + (int32_t)rank_below(m3);
+        else if (sp == 4) row = rb.w + carry3 + (int32_t)rank_below(m4);
+        carry0 += __popcll(m1); carry1 += __popcll(m2);
+        carry2 += __popcll(m3); carry3 += __popcll(m4);
+        if (!active) continue;
+        const size_t r = (size_t)row;
+        const float x = S.x[base + i], y = S.y[base + i];
+        const int32_t h = S.health[base + i];
+        const float s0 = init ? 0.0f : S.sur0[base + i];
+        const float s1 = init ? 0.0f : S.sur1[base + i];
+        const uint32_t st = init ? 0u : S.stats[base + i];
+        S.src_of[r] = S.obsrow[base + i];
+        S.obsrow[base + i] = row;
+        nxt.species[r] = sp;
+        reinterpret_cast<float2 *>(nxt.pos)[r] = make_float2(x, y);
+        nxt.health[r] = h;
+        reinterpret_cast<float2 *>(nxt.sur)[r] = make_float2(s0, s1);
+        const int4 stv = make_int4((int)(st & 1u), (int)((st >> 1) & 1u), (int)((st >> 2) & 1u),
+                                   (int)((st >> 3) & 1u));
+        reinterpret_cast<int4 *>(nxt.stats)[r] = stv;
+        float rv = 0.0f;
+        if (!init) {
+            float sr;
+            if (fixed) sr = sp == 1 ? rew.x : sp == 2 ? rew.y : sp == 3 ? rew.z : rew.w;
+            else sr = sp == 1 ? rew.y : sp == 2 ? rew.z : sp == 3 ? rew.w : next_r0;
+            rv = sr + (float)h / 100.0f - 0.5f;
+            if (stv.z) rv += 10.0f;
+            if (stv.w) rv += 10.0f;
+            if (stv.y) rv += 15.0f;
+        }
+        nxt.reward[r] = rv;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// K4: row move.  For every new row r with old row o = src_of[r] (-1: a newborn
+// or respawned agent, zero-filled -- SURVEY B.13) copy the columns that travel
+// with the observation row: Action, HiddenState, every Prev* column and the
+// prev sensor (semantic, and depth when it is not aliased).  One grid-stride
+// stream of 8/16-byte items over the new rows, so stores are fully coalesced
+// and the gathered loads are contiguous wherever old rows are (most agents
+// keep their species and relative order).
+// ---------------------------------------------------------------------------
+struct MoveSeg {
+    void *dst;
+    const void *src;
+    uint32_t width;   // bytes per item: 4, 8 or 16
+    uint32_t ipr;     // items per row
+};
+constexpr int kMaxMoveSegs = 13;
+struct MoveArgs {
+    MoveSeg seg[kMaxMoveSegs];
+    int nseg;
+};
+
+template <typename T>
+__device__ __forceinline__ void move_item(const MoveSeg &sg, uint32_t idx, int32_t o, uint32_t part)
+{
+    T v{};
+    if (o >= 0) v = reinterpret_cast<const T *>(sg.src)[(size_t)o * sg.ipr + part];
+    reinterpret_cast<T *>(sg.dst)[idx] = v;
+}
+
+__global__ __launch_bounds__(256) void move_kernel(const uint32_t *totals, const int32_t *src_of,
+                                                   MoveArgs args)
+{
+    const uint32_t N = totals[0];
+    const MoveSeg &sg = args.seg[blockIdx.y];
+    const uint32_t items = N * sg.ipr;
+    const uint32_t stride = gridDim.x * blockDim.x;
+    for (uint32_t idx = blockIdx.x * blockDim.x + threadIdx.x; idx < items; idx += stride) {
+        uint32_t r = idx, part = 0;
+        if (sg.ipr == 2) { r = idx >> 1; part = idx & 1u; }
+        else if (sg.ipr == 3) { r = idx / 3u; part = idx - r * 3u; }
+        else if (sg.ipr == 4) { r = idx >> 2; part = idx & 3u; }
+        const int32_t o = src_of[r];
+        if (sg.width == 16) move_item<uint4>(sg, idx, o, part);
+        else if (sg.width == 8) move_item<uint2>(sg, idx, o, part);
+        else move_item<uint32_t>(sg, idx, o, part);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// K3b sensor: 32-pixel raycast (24 forward + 8 backward) plus the finder ray
 // (Madrona RenderingSystem, sim.cpp:1183-1188).  Build spec:
 // objects are unit circles; in an agent's frame (f along heading h, l along
 // r = (hy, -hx)) ray h + u r meets a circle iff
 //     q(u) = (A u - 2 l f) u + C <= 0,   A = f^2 - 1,  C = l^2 - 1,
 // ahead of the origin iff f + u l > 0 (backward camera: < 0); view depth
-// z = f - 1 (>= 0); walls: the ray's exit from the inner arena rectangle.
-// Each ray takes the lexicographic minimum of (z, order) with order = wall 0,
-// food 1 + k, agents 64 + slot.
+// z = f - 1 (>= 0, 15-bit mantissa).  Per ray the lexicographic minimum of
+// (z, order) over objects (food 1 + k, agents 64 + slot) is seen iff it beats
+// the wall (z * d < X - o per axis), else the wall (order 0).
 //
-// One wave per world, agents in chunks of kKeyAgents:
-//  A1  flattened (agent, object) pairs; a wedge test |l| <= |f| + sqrt(2)
-//      (necessary for any hit with |u| < 1) compacts survivors into a queue;
-//  A2  per survivor: approximate roots of q bound the candidate pixels; the
-//      exact predicate runs on those only and ds_min_u64's (z_bits, order)
-//      into the ray key.  Objects that cover many pixels (near, or |f| small)
-//      are evaluated on all 33 rays by the whole wave;
-//  out per (agent, ray): wall depth vs key -> semantic / depth bytes, finder.
-// The exact predicate and depths are evaluated with the same float
-// expressions as oracle/mbots_oracle.c; culling only skips rays it proves
-// cannot pass the predicate.
+// One wave per world, agents in chunks of kKeyAgents; per chunk:
+//  pairs  every (agent, object) pair, one per lane, branch-light: approximate
+//         roots of q bound the candidate pixels; the exact predicate runs on
+//         (at most) 3 candidates + the finder and ds_min_u32's the 32-bit key
+//         (z with its low 8 mantissa bits replaced by the object order);
+//         pairs near the agent or covering more pixels go to a wide list that
+//         the whole wave evaluates on all 33 rays;
+//  output per (agent, ray): key vs wall -> semantic / depth bytes; finder.
+// The exact predicate and depths use the same float expressions as
+// oracle/mbots_oracle.c; culling only skips rays it proves cannot pass.
 // ---------------------------------------------------------------------------
-constexpr int kKeyAgents = 8;                 // agents per chunk (key rows)
-constexpr int kQueue = 128;                   // survivor queue entries
-constexpr float kWedge = 1.41421356f + 0.05f; // |l| <= |f| + sqrt(2) (+ margin)
+#ifndef MB_KEY_AGENTS
+#define MB_KEY_AGENTS 16
+#endif
+#ifndef MB_ABL
+#define MB_ABL 0                              // timing ablations: 1 no sensor work, 8 no output
+#endif
+constexpr int kKeyAgents = MB_KEY_AGENTS;     // agents per chunk (key rows)
+constexpr int kWideCap = 128;                 // wide-pair list (flushed above 64)
+constexpr int kMaxFood = kFoodCap + 2;        // live packages == currentNumFood <= 30
+constexpr float kWedge = 1.41421356f + 0.05f; // |l| <= |f| + sqrt(2): necessary for |u| < 1
 constexpr float kUEps = 2e-3f;                // root-interval margin in u
 constexpr uint32_t kOrderFood = 1u;           // object order: wall 0, food 1.., agents 64..
 constexpr uint32_t kOrderAgent = 64u;
-constexpr unsigned long long kNoHit = ~0ull;
+constexpr uint32_t kNoKey = 0xFFFFFFFFu;
 
 struct SensorLDS {
     float ox[kMaxFood + kMaxCap], oy[kMaxFood + kMaxCap];   // food then agents
     float hx[kMaxCap], hy[kMaxCap];
     int32_t sp[kMaxCap];
     int32_t row[kMaxCap];                                   // new export row per slot
-    unsigned long long key[kKeyAgents * kRays];
-    uint32_t queue[kQueue];
+    uint32_t key[kKeyAgents * kRays];
+    uint32_t wide[kWideCap];
     float u[kSensor];
 };
 
@@ -549,30 +668,21 @@ __constant__ float kURay[kSensor] = {MB_U4(0),  MB_U4(4),  MB_U4(8),  MB_U4(12),
 #undef MB_U4
 
 __device__ __forceinline__ float max0(float x) { return x > 0.0f ? x : 0.0f; }
-
-__device__ __forceinline__ unsigned long long make_key(float z, uint32_t order)
+__device__ __forceinline__ float zq(float z) { return __uint_as_float(__float_as_uint(z) & ~0xFFu); }
+__device__ __forceinline__ uint32_t zkey(float z, uint32_t order)
 {
-    return ((unsigned long long)__float_as_uint(z) << 32) | order;
+    return (__float_as_uint(z) & ~0xFFu) | order;
 }
 
-// wall depth of ray k: exit from the inner rectangle; 0 inside a wall box
-__device__ __forceinline__ float wall_z(const SensorLDS &L, int k, float ox, float oy, float hx,
-                                        float hy)
+__device__ __forceinline__ bool inside_arena(float ox, float oy)
 {
-    float dx, dy;
-    if (k < 24) {
-        const float u = L.u[k];
-        dx = hx + u * hy;
-        dy = hy + u * (-hx);
-    } else if (k < kSensor) {
-        const float u = L.u[k];
-        dx = -(hx + u * hy);
-        dy = -(hy + u * (-hx));
-    } else {
-        dx = hx;
-        dy = hy;
-    }
-    if (!(ox >= kInLo && ox <= kInHiX && oy >= kInLo && oy <= kInHiY)) return 0.0f;
+    return ox >= kInLo && ox <= kInHiX && oy >= kInLo && oy <= kInHiY;
+}
+
+// wall depth of a ray: exit from the inner rectangle; 0 inside a wall box
+__device__ __forceinline__ float wall_z(float ox, float oy, float dx, float dy)
+{
+    if (!inside_arena(ox, oy)) return 0.0f;
     float tx = __builtin_inff(), ty = __builtin_inff();
     if (dx > 0.0f) tx = (kInHiX - ox) / dx;
     else if (dx < 0.0f) tx = (kInLo - ox) / dx;
@@ -582,119 +692,46 @@ __device__ __forceinline__ float wall_z(const SensorLDS &L, int k, float ox, flo
     return t == 0.0f ? 0.0f : t;
 }
 
-// exact predicate of object (f, l) on ray k; returns the key or kNoHit
-__device__ __forceinline__ unsigned long long ray_hit(const SensorLDS &L, int k, float f, float l,
-                                                      float A, float B2, float C, uint32_t order)
+// object at view depth z hides the wall iff z * d < (X - o) per axis
+__device__ __forceinline__ bool beats_wall(float ox, float oy, float dx, float dy, float z)
 {
-    if (k < kSensor) {
-        const float u = L.u[k];
-        const float q = (A * u - B2) * u + C;
-        const float p = f + u * l;
-        if (q <= 0.0f) {
-            if (k < 24) { if (p > 0.0f) return make_key(max0(f - 1.0f), order); }
-            else if (p < 0.0f) return make_key(max0(-f - 1.0f), order);
-        }
-        return kNoHit;
-    }
-    if (C <= 0.0f && f > 0.0f) return make_key(max0(f - 1.0f), order);
-    return kNoHit;
+    const bool bx = dx > 0.0f ? (z * dx < kInHiX - ox) : (dx < 0.0f ? (z * dx > kInLo - ox) : true);
+    const bool by = dy > 0.0f ? (z * dy < kInHiY - oy) : (dy < 0.0f ? (z * dy > kInLo - oy) : true);
+    return inside_arena(ox, oy) && bx && by;
 }
 
-__device__ __forceinline__ void pair_frame(const SensorLDS &L, int nf, int i, int j, float &f,
-                                           float &l)
-{
-    const float vx = L.ox[j] - L.ox[nf + i], vy = L.oy[j] - L.oy[nf + i];
-    const float hx = L.hx[i], hy = L.hy[i];
-    f = vx * hx + vy * hy;
-    l = vx * hy - vy * hx;
-}
-
-// A2 over queue entries [q0, q0 + cnt) (cnt <= 64)
-__device__ __forceinline__ void process_queue(SensorLDS &L, int a0, int nf, int q0, int cnt)
+// the whole wave evaluates one wide pair (agent ic of the chunk, object j) on
+// rays 0..32 (lane = ray)
+__device__ __forceinline__ void wide_pair(SensorLDS &L, int a0, int nf, uint32_t code)
 {
     const int lane = (int)__lane_id();
-    bool wide = false;
-    float f = 0.f, l = 0.f, A = 0.f, B2 = 0.f, C = 0.f;
-    uint32_t order = 0, ii = 0;
-    if (lane < cnt) {
-        const uint32_t e = L.queue[q0 + lane];
-        ii = e & 0xFFu;
-        const int j = (int)(e >> 8);
-        order = j < nf ? kOrderFood + (uint32_t)j : kOrderAgent + (uint32_t)(j - nf);
-        pair_frame(L, nf, a0 + (int)ii, j, f, l);
-        const float r2 = f * f + l * l;
-        A = f * f - 1.0f;
-        B2 = 2.0f * (l * f);
-        C = l * l - 1.0f;
-        unsigned long long *key = L.key + ii * kRays;
-        if (r2 <= 1.0f || fabsf(f) <= 1.5f) {
-            wide = true;
-        } else {
-            // approximate roots of q bound the candidate pixels
-            const float sq = __builtin_amdgcn_sqrtf(r2 - 1.0f);
-            const float ia = __builtin_amdgcn_rcpf(A);
-            const float u1 = (l * f - sq) * ia - kUEps, u2 = (l * f + sq) * ia + kUEps;
-            int k0, k1;
-            if (f > 0.0f) {
-                k0 = (int)ceilf(fmaxf((u1 + 1.0f) * 12.0f - 0.5f, -1.0f));
-                k1 = (int)floorf(fminf((u2 + 1.0f) * 12.0f - 0.5f, 24.0f));
-                k0 = max(k0, 0);
-                k1 = min(k1, 23);
-            } else {
-                k0 = (int)ceilf(fmaxf((u1 + 1.0f) * 4.0f - 0.5f, -1.0f));
-                k1 = (int)floorf(fminf((u2 + 1.0f) * 4.0f - 0.5f, 8.0f));
-                k0 = 24 + max(k0, 0);
-                k1 = 24 + min(k1, 7);
-            }
-            const int c = k1 - k0 + 1;
-            if (c > 3) {
-                wide = true;
-            } else {
-#pragma unroll
-                for (int e2 = 0; e2 < 3; ++e2) {
-                    if (e2 < c) {
-                        const unsigned long long kv = ray_hit(L, k0 + e2, f, l, A, B2, C, order);
-                        if (kv != kNoHit) atomicMin(&key[k0 + e2], kv);
-                    }
-                }
-                if (f > 0.0f && u1 <= 0.0f && u2 >= 0.0f) {
-                    const unsigned long long kv = ray_hit(L, kSensor, f, l, A, B2, C, order);
-                    if (kv != kNoHit) atomicMin(&key[kSensor], kv);
-                }
-            }
-        }
+    const int ic = (int)(code & 0xFFu), j = (int)(code >> 8);
+    const int i = a0 + ic;
+    const float hx = L.hx[i], hy = L.hy[i];
+    const float vx = L.ox[j] - L.ox[nf + i], vy = L.oy[j] - L.oy[nf + i];
+    const float f = vx * hx + vy * hy;
+    const float l = vx * hy - vy * hx;
+    const uint32_t order = j < nf ? kOrderFood + (uint32_t)j : kOrderAgent + (uint32_t)(j - nf);
+    const float r2 = f * f + l * l;
+    const float A = f * f - 1.0f, B2 = 2.0f * (l * f), C = l * l - 1.0f;
+    bool hit;
+    float z;
+    if (lane < kSensor) {
+        const float u = L.u[lane];
+        const float q = (A * u - B2) * u + C;
+        const float p = f + u * l;
+        const bool fwdk = lane < 24;
+        hit = q <= 0.0f && (fwdk ? p > 0.0f : p < 0.0f);
+        z = zq(max0(fwdk ? f - 1.0f : -f - 1.0f));
+    } else {
+        hit = C <= 0.0f && f > 0.0f;
+        z = zq(max0(f - 1.0f));
     }
-    // wide objects: the whole wave evaluates all 33 rays of each
-    uint64_t wm = ballot64(wide);
-    while (wm) {
-        const int src = __builtin_ctzll(wm);
-        wm &= wm - 1;
-        const float wf = __shfl(f, src), wl = __shfl(l, src);
-        const float wA = __shfl(A, src), wB2 = __shfl(B2, src), wC = __shfl(C, src);
-        const uint32_t word = (uint32_t)__shfl((int)order, src);
-        const uint32_t wii = (uint32_t)__shfl((int)ii, src);
-        const float r2 = wf * wf + wl * wl;
-        if (lane <= kSensor) {
-            const unsigned long long kv = r2 <= 1.0f ? make_key(0.0f, word)
-                                                     : ray_hit(L, lane, wf, wl, wA, wB2, wC, word);
-            if (kv != kNoHit) atomicMin(&L.key[wii * kRays + lane], kv);
-        }
-    }
+    if (r2 <= 1.0f) { hit = true; z = 0.0f; }
+    if (lane <= kSensor && hit) atomicMin(&L.key[ic * kRays + lane], zkey(z, order));
 }
 
-
-// ---------------------------------------------------------------------------
-// K3: export + sensor, one wave per world.
-//  * updateObservations (sim.cpp:687-717) into the world's species-major rows
-//    of the next table, carrying Action / HiddenState / Prev* from the old row
-//    (the obs row travels through the species sort), updateSensorOutputIdx's
-//    prev-sensor copy (sim.cpp:736-789), rewardSystem setting 8
-//    (sim.cpp:840-983, faithful rewards[speciesID] off-by-one unless fixed);
-//  * then the raycast sensor (Sensor graph, sim.cpp:1183-1188) into the new
-//    rows, and the finder slot for the next step's shoot / breed.
-// ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void export_sensor_kernel(SimState S, ObsTable cur,
-                                                            ObsTable nxt, int init)
+__global__ __launch_bounds__(256) void sensor_kernel(SimState S, ObsTable nxt)
 {
     __shared__ SensorLDS lds[kWorldsPerBlock];
     const uint32_t wv = threadIdx.x >> 6;
@@ -737,189 +774,123 @@ __global__ __launch_bounds__(256) void export_sensor_kernel(SimState S, ObsTable
         }
         nf = min(tot, kMaxFood);
     }
-
-    // ---- export rows ----
-    const int4 rb = reinterpret_cast<const int4 *>(S.row_base)[w];
-    const float4 rew = reinterpret_cast<const float4 *>(S.sreward)[w];
-    const bool fixed = (S.flags & kFlagRewardFixed) != 0;
-    // faithful B.3: rewards[4] reads the next SpeciesInfo row's rewards[0]
-    const float next_r0 = (w + 1 < S.W) ? S.sreward[(size_t)(w + 1) * kNumSpecies] : 0.0f;
-    int carry0 = 0, carry1 = 0, carry2 = 0, carry3 = 0;
-    for (int b = 0; b < n; b += 64) {
-        const int i = b + (int)lane;
-        const bool active = i < n;
-        const int32_t sp = active ? S.species[base + i] : 0;
-        const uint64_t m1 = ballot64(sp == 1), m2 = ballot64(sp == 2);
-        const uint64_t m3 = ballot64(sp == 3), m4 = ballot64(sp == 4);
-        int32_t row = 0;
-        if (sp == 1) row = rb.x + carry0 + (int32_t)rank_below(m1);
-        else if (sp == 2) row = rb.y + carry1 + (int32_t)rank_below(m2);
-        else if (sp == 3) row = rb.z + carry2 + (int32_t)rank_below(m3);
-        else if (sp == 4) row = rb.w + carry3 + (int32_t)rank_below(m4);
-        carry0 += __popcll(m1); carry1 += __popcll(m2);
-        carry2 += __popcll(m3); carry3 += __popcll(m4);
-        if (!active) continue;
-
-        const size_t r = (size_t)row;
-        const float x = S.x[base + i], y = S.y[base + i];
-        const int32_t h = S.health[base + i];
-        const float s0 = init ? 0.0f : S.sur0[base + i];
-        const float s1 = init ? 0.0f : S.sur1[base + i];
-        const uint32_t st = init ? 0u : S.stats[base + i];
-        const int32_t orow = S.obsrow[base + i];
-        {
-            float hx, hy;
-            heading(S.rw[base + i], S.rz[base + i], hx, hy);
-            L.ox[nf + i] = x;
-            L.oy[nf + i] = y;
-            L.sp[i] = sp;
-            L.hx[i] = hx;
-            L.hy[i] = hy;
-            L.row[i] = row;
-        }
-
-        nxt.species[r] = sp;
-        reinterpret_cast<float2 *>(nxt.pos)[r] = make_float2(x, y);
-        nxt.health[r] = h;
-        reinterpret_cast<float2 *>(nxt.sur)[r] = make_float2(s0, s1);
-        const int4 stv = make_int4((int)(st & 1u), (int)((st >> 1) & 1u), (int)((st >> 2) & 1u),
-                                   (int)((st >> 3) & 1u));
-        reinterpret_cast<int4 *>(nxt.stats)[r] = stv;
-        float rv = 0.0f;
-        if (!init) {
-            float sr;
-            if (fixed) sr = sp == 1 ? rew.x : sp == 2 ? rew.y : sp == 3 ? rew.z : rew.w;
-            else sr = sp == 1 ? rew.y : sp == 2 ? rew.z : sp == 3 ? rew.w : next_r0;
-            rv = sr + (float)h / 100.0f - 0.5f;
-            if (stv.z) rv += 10.0f;
-            if (stv.w) rv += 10.0f;
-            if (stv.y) rv += 15.0f;
-        }
-        nxt.reward[r] = rv;
-        S.obsrow[base + i] = row;
-
-        int2 *nap = reinterpret_cast<int2 *>(nxt.action + r * 6);
-        float4 *nhp = reinterpret_cast<float4 *>(nxt.hidden + r * kHidden);
-        int2 *npap = reinterpret_cast<int2 *>(nxt.paction + r * 6);
-        float4 *nphp = reinterpret_cast<float4 *>(nxt.phidden + r * kHidden);
-        uint4 *nps = reinterpret_cast<uint4 *>(nxt.psem + r * kSensor);
-        if (orow >= 0) {
-            const size_t o = (size_t)orow;
-            const int2 *ap = reinterpret_cast<const int2 *>(cur.action + o * 6);
-            nap[0] = ap[0]; nap[1] = ap[1]; nap[2] = ap[2];
-            const float4 *hp = reinterpret_cast<const float4 *>(cur.hidden + o * kHidden);
-            nhp[0] = hp[0]; nhp[1] = hp[1]; nhp[2] = hp[2]; nhp[3] = hp[3];
-            nxt.pspecies[r] = cur.pspecies[o];
-            reinterpret_cast<float2 *>(nxt.ppos)[r] = reinterpret_cast<const float2 *>(cur.ppos)[o];
-            nxt.phealth[r] = cur.phealth[o];
-            reinterpret_cast<float2 *>(nxt.psur)[r] = reinterpret_cast<const float2 *>(cur.psur)[o];
-            nxt.preward[r] = cur.preward[o];
-            const int2 *pap = reinterpret_cast<const int2 *>(cur.paction + o * 6);
-            npap[0] = pap[0]; npap[1] = pap[1]; npap[2] = pap[2];
-            reinterpret_cast<int4 *>(nxt.pstats)[r] = reinterpret_cast<const int4 *>(cur.pstats)[o];
-            const float4 *php = reinterpret_cast<const float4 *>(cur.phidden + o * kHidden);
-            nphp[0] = php[0]; nphp[1] = php[1]; nphp[2] = php[2]; nphp[3] = php[3];
-            const uint4 *sp4 = reinterpret_cast<const uint4 *>(cur.sem + o * kSensor);
-            nps[0] = sp4[0]; nps[1] = sp4[1];
-            if (depth) {
-                const uint4 *dp4 = reinterpret_cast<const uint4 *>(cur.depth + o * kSensor);
-                uint4 *npd = reinterpret_cast<uint4 *>(nxt.pdepth + r * kSensor);
-                npd[0] = dp4[0]; npd[1] = dp4[1];
-            }
-        } else {
-            const int2 z2 = make_int2(0, 0);
-            const float4 z4 = make_float4(0.f, 0.f, 0.f, 0.f);
-            const uint4 zu = make_uint4(0u, 0u, 0u, 0u);
-            nap[0] = z2; nap[1] = z2; nap[2] = z2;
-            nhp[0] = z4; nhp[1] = z4; nhp[2] = z4; nhp[3] = z4;
-            nxt.pspecies[r] = 0;
-            reinterpret_cast<float2 *>(nxt.ppos)[r] = make_float2(0.f, 0.f);
-            nxt.phealth[r] = 0;
-            reinterpret_cast<float2 *>(nxt.psur)[r] = make_float2(0.f, 0.f);
-            nxt.preward[r] = 0.0f;
-            npap[0] = z2; npap[1] = z2; npap[2] = z2;
-            reinterpret_cast<int4 *>(nxt.pstats)[r] = make_int4(0, 0, 0, 0);
-            nphp[0] = z4; nphp[1] = z4; nphp[2] = z4; nphp[3] = z4;
-            nps[0] = zu; nps[1] = zu;
-            if (depth) {
-                uint4 *npd = reinterpret_cast<uint4 *>(nxt.pdepth + r * kSensor);
-                npd[0] = zu; npd[1] = zu;
-            }
-        }
+    for (int i = lane; i < n; i += 64) {
+        float hx, hy;
+        heading(S.rw[base + i], S.rz[base + i], hx, hy);
+        L.ox[nf + i] = S.x[base + i];
+        L.oy[nf + i] = S.y[base + i];
+        L.sp[i] = S.species[base + i];
+        L.hx[i] = hx;
+        L.hy[i] = hy;
+        L.row[i] = S.obsrow[base + i];
     }
-    if (init) return;
+    if (MB_ABL & 1) return;
     const int nobj = nf + n;
+    const float inv_nobj = 1.0f / (float)nobj;
     wave_sync();
+
     for (int a0 = 0; a0 < n; a0 += kKeyAgents) {
         const int nc = min(kKeyAgents, n - a0);
-        for (int q = lane; q < nc * kRays; q += 64) L.key[q] = kNoHit;
+        for (int q = lane; q < nc * kRays; q += 64) L.key[q] = kNoKey;
         wave_sync();
-        // ---- A1: wedge pre-cull of flattened pairs into the queue ----
-        int nq = 0;
-        int ii = 0, j = (int)lane;
-        while (j >= nobj) { j -= nobj; ++ii; }
+        // ---- pairs ----
         const int npairs = nc * nobj;
+        int nw = 0;
         for (int qb = 0; qb < npairs; qb += 64) {
-            bool keep = false;
-            if (ii < nc && j != nf + a0 + ii) {
-                float f, l;
-                pair_frame(L, nf, a0 + ii, j, f, l);
-                keep = fabsf(l) <= fabsf(f) + kWedge;
+            const int q = qb + (int)lane;
+            int ii = (int)((float)q * inv_nobj);
+            int j = q - ii * nobj;
+            ii = j < 0 ? ii - 1 : (j >= nobj ? ii + 1 : ii);
+            j = q - ii * nobj;
+            const int ic = min(ii, nc - 1);
+            const int i = a0 + ic;
+            const bool valid = q < npairs && j != nf + i;
+            const float hx = L.hx[i], hy = L.hy[i];
+            const float vx = L.ox[j] - L.ox[nf + i], vy = L.oy[j] - L.oy[nf + i];
+            const float f = vx * hx + vy * hy;   // along the heading
+            const float l = vx * hy - vy * hx;   // along r = (hy, -hx)
+            const uint32_t order = j < nf ? kOrderFood + (uint32_t)j : kOrderAgent + (uint32_t)(j - nf);
+            const float r2 = f * f + l * l;
+            const float A = f * f - 1.0f, B2 = 2.0f * (l * f), C = l * l - 1.0f;
+            const bool inwedge = valid && fabsf(l) <= fabsf(f) + kWedge;
+            // approximate roots bound the candidate pixels of the camera it faces
+            const bool fwd = f > 0.0f;
+            const float sq = __builtin_amdgcn_sqrtf(fmaxf(r2 - 1.0f, 0.0f));
+            const float ia = __builtin_amdgcn_rcpf(A);
+            const float u1 = (l * f - sq) * ia - kUEps, u2 = (l * f + sq) * ia + kUEps;
+            const float sc = fwd ? 12.0f : 4.0f, kmax = fwd ? 23.0f : 7.0f;
+            const float lo = fmaxf((u1 + 1.0f) * sc - 0.5f, -1.0f);
+            const float hi = fminf((u2 + 1.0f) * sc - 0.5f, kmax + 1.0f);
+            const int k0 = max((int)ceilf(lo), 0), k1 = min((int)floorf(hi), (int)kmax);
+            const int c = k1 - k0 + 1;
+            const bool wide = inwedge && (r2 <= 1.0f || fabsf(f) <= 1.5f || c > 3);
+            const bool narrow = inwedge && !wide;
+            const float z = zq(max0(fwd ? f - 1.0f : -f - 1.0f));
+            const uint32_t key = zkey(z, order);
+            uint32_t *kr = L.key + ic * kRays;
+            const int kb = fwd ? 0 : 24;
+#pragma unroll
+            for (int e = 0; e < 3; ++e) {
+                const int k = kb + min(k0 + e, (int)kmax);
+                const float u = L.u[k];
+                const float qv = (A * u - B2) * u + C;
+                const float p = f + u * l;
+                const bool hit = narrow && e < c && qv <= 0.0f && (fwd ? p > 0.0f : p < 0.0f);
+                if (hit) atomicMin(&kr[k], key);
             }
-            const uint64_t m = ballot64(keep);
-            if (keep) L.queue[nq + (int)rank_below(m)] = (uint32_t)ii | ((uint32_t)j << 8);
-            nq += __popcll(m);
-            if (nq >= 64) {
+            if (narrow && fwd && C <= 0.0f) atomicMin(&kr[kSensor], key);   // finder ray
+            const uint64_t wm = ballot64(wide);
+            if (wide) L.wide[nw + (int)rank_below(wm)] = (uint32_t)ic | ((uint32_t)j << 8);
+            nw += __popcll(wm);
+            if (nw > kWideCap - 64) {
                 wave_sync();
-                process_queue(L, a0, nf, nq - 64, 64);
-                wave_sync();
-                nq -= 64;
+                for (int e = 0; e < nw; ++e) wide_pair(L, a0, nf, L.wide[e]);
+                nw = 0;
             }
-            j += 64;
-            while (j >= nobj) { j -= nobj; ++ii; }
-        }
-        if (nq > 0) {
-            wave_sync();
-            process_queue(L, a0, nf, 0, nq);
         }
         wave_sync();
-        // ---- output: walls vs keys, two agents per wave ----
-        for (int pb = 0; pb < nc; pb += 2) {
+        for (int e = 0; e < nw; ++e) wide_pair(L, a0, nf, L.wide[e]);
+        wave_sync();
+        // ---- output: keys vs walls, two agents per wave ----
+        for (int pb = 0; pb < ((MB_ABL & 8) ? 0 : nc); pb += 2) {
             const int ci = pb + (int)(lane >> 5);
             const int px = (int)(lane & 31u);
             const bool valid = ci < nc;
-            uint32_t semv = 0u, depv = 0u;
-            if (valid) {
-                const int i = a0 + ci;
-                const float wz = wall_z(L, px, L.ox[nf + i], L.oy[nf + i], L.hx[i], L.hy[i]);
-                unsigned long long kv = L.key[ci * kRays + px];
-                const unsigned long long kw = make_key(wz, 0u);
-                if (kw < kv) kv = kw;
-                const uint32_t order = (uint32_t)kv;
-                const int sem = order == 0u ? 5 : (order < kOrderAgent ? 6 : L.sp[order - kOrderAgent]);
-                semv = (uint32_t)(uint8_t)(int8_t)sem;
-                depv = depth_u8(__uint_as_float((uint32_t)(kv >> 32)));
-            }
-            semv <<= 8u * (lane & 3u);
-            depv <<= 8u * (lane & 3u);
+            const int i = a0 + min(ci, nc - 1);
+            const float ox = L.ox[nf + i], oy = L.oy[nf + i], hx = L.hx[i], hy = L.hy[i];
+            const float u = L.u[px];
+            const float sgn = px < 24 ? 1.0f : -1.0f;
+            const float dx = sgn * (hx + u * hy), dy = sgn * (hy + u * (-hx));
+            const uint32_t kv = L.key[min(ci, nc - 1) * kRays + px];
+            const float oz = __uint_as_float(kv & ~0xFFu);
+            const uint32_t order = kv & 0xFFu;
+            const bool obj = kv != kNoKey && beats_wall(ox, oy, dx, dy, oz);
+            const int spv = L.sp[min((int)(order - kOrderAgent), n - 1) & 127];
+            const int sem = obj ? (order < kOrderAgent ? 6 : spv) : 5;
+            float z = oz;
+            if (!obj) z = depth ? wall_z(ox, oy, dx, dy) : 0.0f;
+            uint32_t semv = (uint32_t)(uint8_t)(int8_t)sem << (8u * (lane & 3u));
+            uint32_t depv = (uint32_t)depth_u8(z) << (8u * (lane & 3u));
             semv |= __shfl_xor(semv, 1);
             semv |= __shfl_xor(semv, 2);
-            depv |= __shfl_xor(depv, 1);
-            depv |= __shfl_xor(depv, 2);
+            if (depth) {
+                depv |= __shfl_xor(depv, 1);
+                depv |= __shfl_xor(depv, 2);
+            }
             if (valid && (lane & 3u) == 0u) {
-                const size_t r = (size_t)L.row[a0 + ci];
+                const size_t r = (size_t)L.row[i];
                 reinterpret_cast<uint32_t *>(nxt.sem + r * kSensor)[px >> 2] = semv;
                 if (depth) reinterpret_cast<uint32_t *>(nxt.depth + r * kSensor)[px >> 2] = depv;
             }
         }
         if ((int)lane < nc) {
             const int i = a0 + (int)lane;
-            const float wz = wall_z(L, kSensor, L.ox[nf + i], L.oy[nf + i], L.hx[i], L.hy[i]);
-            unsigned long long kv = L.key[lane * kRays + kSensor];
-            const unsigned long long kw = make_key(wz, 0u);
-            if (kw < kv) kv = kw;
-            const uint32_t order = (uint32_t)kv;
-            S.finder[base + i] = order >= kOrderAgent ? (int32_t)(order - kOrderAgent) : -1;
+            const uint32_t kv = L.key[lane * kRays + kSensor];
+            const uint32_t order = kv & 0xFFu;
+            const bool agent = kv != kNoKey && order >= kOrderAgent &&
+                               beats_wall(L.ox[nf + i], L.oy[nf + i], L.hx[i], L.hy[i],
+                                          __uint_as_float(kv & ~0xFFu));
+            S.finder[base + i] = agent ? (int32_t)(order - kOrderAgent) : -1;
         }
         wave_sync();
     }
@@ -1072,11 +1043,37 @@ hipError_t launch_scan(const SimState &S, int parity, hipStream_t st)
     hipLaunchKernelGGL(scan_kernel, dim3(S.ntiles), dim3(1024), 0, st, S, parity);
     return hipGetLastError();
 }
-hipError_t launch_export_sensor(const SimState &S, const ObsTable &cur, const ObsTable &nxt,
-                                int init, hipStream_t st)
+hipError_t launch_export_rows(const SimState &S, const ObsTable &nxt, int init, hipStream_t st)
 {
-    hipLaunchKernelGGL(export_sensor_kernel, dim3(world_blocks(S.W)), dim3(256), 0, st, S, cur,
-                       nxt, init);
+    hipLaunchKernelGGL(export_rows_kernel, dim3(world_blocks(S.W)), dim3(256), 0, st, S, nxt, init);
+    return hipGetLastError();
+}
+hipError_t launch_move(const SimState &S, const ObsTable &cur, const ObsTable &nxt, hipStream_t st)
+{
+    MoveArgs m{};
+    int k = 0;
+    auto add = [&](void *d, const void *s, uint32_t width, uint32_t ipr) {
+        m.seg[k++] = MoveSeg{d, s, width, ipr};
+    };
+    add(nxt.action, cur.action, 8, 3);
+    add(nxt.hidden, cur.hidden, 16, 4);
+    add(nxt.pspecies, cur.pspecies, 4, 1);
+    add(nxt.ppos, cur.ppos, 8, 1);
+    add(nxt.phealth, cur.phealth, 4, 1);
+    add(nxt.psur, cur.psur, 8, 1);
+    add(nxt.preward, cur.preward, 4, 1);
+    add(nxt.paction, cur.paction, 8, 3);
+    add(nxt.pstats, cur.pstats, 16, 1);
+    add(nxt.phidden, cur.phidden, 16, 4);
+    add(nxt.psem, cur.sem, 16, 2);                   // prev sensor <- last step's sensor
+    if (S.flags & kFlagFixDepth) add(nxt.pdepth, cur.depth, 16, 2);
+    m.nseg = k;
+    hipLaunchKernelGGL(move_kernel, dim3(512, k), dim3(256), 0, st, S.totals, S.src_of, m);
+    return hipGetLastError();
+}
+hipError_t launch_sensor(const SimState &S, const ObsTable &nxt, hipStream_t st)
+{
+    hipLaunchKernelGGL(sensor_kernel, dim3(world_blocks(S.W)), dim3(256), 0, st, S, nxt);
     return hipGetLastError();
 }
 hipError_t launch_shift(const SimState &S, const ObsTable &t, hipStream_t st)

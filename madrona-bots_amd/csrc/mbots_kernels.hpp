@@ -26,6 +26,7 @@ struct SimState {
     int32_t *scount;                // [W][4] SpeciesCount (exported)
     int32_t *row_base;              // [W][4] first export row of (world, species)
     int32_t *world_off;             // [W] world-major agent offsets
+    int32_t *src_of;                // [W*cap] new export row -> old row (-1: new agent)
     uint32_t *overflow;             // [W] dropped births/respawns
     uint32_t *totals;               // [0] = N, [1..4] = per-species rows
     int32_t *tiles;                 // [2][ntiles][5] per-tile species/agent counts (K1 -> K2)
@@ -47,8 +48,9 @@ hipError_t launch_init(const SimState &S, hipStream_t st);
 hipError_t launch_tile_sum(const SimState &S, int parity, hipStream_t st);
 hipError_t launch_world_step(const SimState &S, const ObsTable &cur, int parity, hipStream_t st);
 hipError_t launch_scan(const SimState &S, int parity, hipStream_t st);
-hipError_t launch_export_sensor(const SimState &S, const ObsTable &cur, const ObsTable &nxt,
-                                int init, hipStream_t st);
+hipError_t launch_export_rows(const SimState &S, const ObsTable &nxt, int init, hipStream_t st);
+hipError_t launch_move(const SimState &S, const ObsTable &cur, const ObsTable &nxt, hipStream_t st);
+hipError_t launch_sensor(const SimState &S, const ObsTable &nxt, hipStream_t st);
 hipError_t launch_shift(const SimState &S, const ObsTable &t, hipStream_t st);
 hipError_t launch_synthetic_actions(const SimState &S, const ObsTable &t, uint32_t seed,
                                     uint32_t step, int write_hidden, hipStream_t st);

@@ -71,6 +71,8 @@ struct mbots_handle {
     int32_t *sensor_index = nullptr;  // scratch for sensorIndexTensor
     uint32_t *h_totals = nullptr;     // pinned mirror of S.totals
     hipEvent_t ev_totals = nullptr;
+    hipStream_t aux = nullptr;        // internal stream: K4 move next to the K3b sensor
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     hipStream_t last_stream = nullptr;
     bool timing = false;
     std::vector<TimedPair> pending;
@@ -160,6 +162,7 @@ size_t layout(mbots_handle *h, Arena &a)
     S.scount = a.take<int32_t>(W * kNumSpecies);
     S.row_base = a.take<int32_t>(W * kNumSpecies);
     S.world_off = a.take<int32_t>(W);
+    S.src_of = a.take<int32_t>(rows);
     S.overflow = a.take<uint32_t>(W);
     S.totals = a.take<uint32_t>(8);
     S.ntiles = scan_tiles((uint32_t)W);
@@ -249,13 +252,17 @@ int mbots_create(const mbots_config *cfg_in, mbots_handle **out)
     check(hipHostMalloc((void **)&h->h_totals, 8 * sizeof(uint32_t), hipHostMallocDefault),
           "hipHostMalloc");
     check(hipEventCreateWithFlags(&h->ev_totals, hipEventDisableTiming), "hipEventCreate");
+    check(hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming), "hipEventCreate");
+    check(hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming), "hipEventCreate");
+    check(hipStreamCreateWithFlags(&h->aux, hipStreamNonBlocking), "hipStreamCreate");
     hipStream_t st = nullptr;
     check(hipMemsetAsync(h->arena.base, 0, bytes, st), "hipMemsetAsync");
     // Sim::Sim / initWorld (sim.cpp:1232-1256) + initial export of the rows
     check(mbots::launch_init(S, st), "init_kernel");
     check(mbots::launch_tile_sum(S, 0, st), "tile_sum_kernel");
     check(mbots::launch_scan(S, 0, st), "scan_kernel");
-    check(mbots::launch_export_sensor(S, h->T[1], h->T[0], 1, st), "export_sensor_kernel(init)");
+    check(mbots::launch_export_rows(S, h->T[0], 1, st), "export_rows_kernel(init)");
+    check(mbots::launch_move(S, h->T[1], h->T[0], st), "move_kernel(init)");
     if (rc == MBOTS_OK) rc = record_totals(h, st);
     check(hipStreamSynchronize(st), "hipStreamSynchronize");
     if (rc != MBOTS_OK) {
@@ -279,6 +286,9 @@ int mbots_destroy(mbots_handle *h)
     for (auto &p : h->pending) { (void)hipEventDestroy(p.a); (void)hipEventDestroy(p.b); }
     for (auto e : h->pool) (void)hipEventDestroy(e);
     if (h->ev_totals) (void)hipEventDestroy(h->ev_totals);
+    if (h->ev_fork) (void)hipEventDestroy(h->ev_fork);
+    if (h->ev_join) (void)hipEventDestroy(h->ev_join);
+    if (h->aux) (void)hipStreamDestroy(h->aux);
     if (h->h_totals) (void)hipHostFree(h->h_totals);
     if (h->arena.base) (void)hipFree(h->arena.base);
     delete h;
@@ -300,8 +310,24 @@ int mbots_step(mbots_handle *h, void *stream)
         return rc;
     if ((rc = timed(h, MBOTS_TK_SCAN, st, [&] { return mbots::launch_scan(h->S, par, st); }))) return rc;
     if ((rc = timed(h, MBOTS_TK_EXPORT, st,
-                    [&] { return mbots::launch_export_sensor(h->S, cur, nxt, 0, st); })))
+                    [&] { return mbots::launch_export_rows(h->S, nxt, 0, st); })))
         return rc;
+#ifdef MB_NO_FORK
+    if ((rc = timed(h, MBOTS_TK_MOVE, st, [&] { return mbots::launch_move(h->S, cur, nxt, st); })))
+        return rc;
+    if ((rc = timed(h, MBOTS_TK_SENSOR, st, [&] { return mbots::launch_sensor(h->S, nxt, st); })))
+        return rc;
+#else
+    // fork: K4 move (HBM stream) on the aux stream || K3b sensor (VALU) on st
+    HIP_TRY(hipEventRecord(h->ev_fork, st));
+    HIP_TRY(hipStreamWaitEvent(h->aux, h->ev_fork, 0));
+    if ((rc = timed(h, MBOTS_TK_MOVE, h->aux, [&] { return mbots::launch_move(h->S, cur, nxt, h->aux); })))
+        return rc;
+    HIP_TRY(hipEventRecord(h->ev_join, h->aux));
+    if ((rc = timed(h, MBOTS_TK_SENSOR, st, [&] { return mbots::launch_sensor(h->S, nxt, st); })))
+        return rc;
+    HIP_TRY(hipStreamWaitEvent(st, h->ev_join, 0));
+#endif
     h->parity ^= 1;
     h->tb ^= 1;
     return record_totals(h, st);

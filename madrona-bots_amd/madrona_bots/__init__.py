@@ -24,7 +24,8 @@ import torch  # loads the HIP runtime libmbots.so links against (same soname)
 __all__ = ["SimManager", "Tensor", "madrona", "ExportID"]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-_LIB_PATH = os.path.join(_HERE, "libmbots.so")
+# MBOTS_LIB: developer override to A/B alternative builds of the same library
+_LIB_PATH = os.environ.get("MBOTS_LIB") or os.path.join(_HERE, "libmbots.so")
 
 if not os.path.exists(_LIB_PATH):
     raise ImportError(
@@ -97,7 +98,7 @@ FLAG_REWARD_FIXED = 0x1
 FLAG_FIX_DEPTH_ALIAS = 0x2
 
 # TK_* indices of mbots_kernel_times
-KERNELS = ("world_step", "scan", "export", "sensor", "shift", "actions")
+KERNELS = ("world_step", "scan", "export", "sensor", "shift", "actions", "move")
 
 
 class Tensor:

@@ -517,7 +517,8 @@ static void world_phase_c(orc_sim *s, uint32_t wi)
 /* the heading h, l along r = (hy, -hx)) the ray direction h + u r meets the  */
 /* circle iff q(u) = (A u - 2 l f) u + C <= 0 with A = f^2 - 1, C = l^2 - 1,  */
 /* and the hit lies ahead of the ray iff f + u l > 0 (backward camera: < 0).  */
-/* Depth is view-space z: z = f - 1 (clamped at 0) for circles, the ray's     */
+/* Depth is view-space z: z = f - 1 (clamped at 0, 15-bit mantissa: zq) for  */
+/* circles, the ray's                                                        */
 /* exit from the inner arena rectangle for the walls.  Each pixel takes the   */
 /* lexicographic minimum of (z, order): walls 0, food 1 + k, agents 64 + slot.*/
 /* ------------------------------------------------------------------------ */
@@ -563,6 +564,30 @@ static float wall_z(float ox, float oy, float dx, float dy)
 
 static inline float max0(float x) { return x > 0.0f ? x : 0.0f; }
 
+/* object depths keep 15 mantissa bits (the low 8 carry the object order in
+ * the HIP kernel's 32-bit z-buffer key); floor(z) is unchanged for z < 2^15 */
+static inline float zq(float z)
+{
+    uint32_t b;
+    memcpy(&b, &z, 4);
+    b &= ~0xFFu;
+    memcpy(&z, &b, 4);
+    return z;
+}
+
+/* An object at view depth z hides the wall on ray (dx, dy) iff the ray meets
+ * it strictly before leaving the inner rectangle, tested as z * d < (X - o)
+ * per axis (no division); an origin inside a wall box sees the wall (z 0). */
+static int beats_wall(float ox, float oy, float dx, float dy, float z)
+{
+    if (!(ox >= kInLo && ox <= kInHiX && oy >= kInLo && oy <= kInHiY)) return 0;
+    if (dx > 0.0f) { if (!(z * dx < kInHiX - ox)) return 0; }
+    else if (dx < 0.0f) { if (!(z * dx > kInLo - ox)) return 0; }
+    if (dy > 0.0f) { if (!(z * dy < kInHiY - oy)) return 0; }
+    else if (dy < 0.0f) { if (!(z * dy > kInLo - oy)) return 0; }
+    return 1;
+}
+
 typedef struct { float z; uint32_t order; } orc_hit;
 
 static inline void consider(orc_hit *h, float z, uint32_t order)
@@ -583,15 +608,16 @@ static void raster(orc_hit *hits, float ax, float ay, float hx, float hy, float 
         return;
     }
     float A = f * f - 1.0f, B2 = 2.0f * (l * f), C = l * l - 1.0f;
+    float zf = zq(max0(f - 1.0f)), zb = zq(max0(-f - 1.0f));
     for (int k = 0; k < ORC_SENSOR; ++k) {
         float u = ray_u(k);
         float q = (A * u - B2) * u + C;
         float p = f + u * l;
         if (!(q <= 0.0f)) continue;
-        if (k < 24) { if (p > 0.0f) consider(&hits[k], max0(f - 1.0f), order); }
-        else { if (p < 0.0f) consider(&hits[k], max0(-f - 1.0f), order); }
+        if (k < 24) { if (p > 0.0f) consider(&hits[k], zf, order); }
+        else { if (p < 0.0f) consider(&hits[k], zb, order); }
     }
-    if (C <= 0.0f && f > 0.0f) consider(&hits[ORC_SENSOR], max0(f - 1.0f), order);
+    if (C <= 0.0f && f > 0.0f) consider(&hits[ORC_SENSOR], zf, order);
 }
 
 static inline uint8_t depth_u8(float t)
@@ -610,10 +636,8 @@ static void world_phase_d(orc_sim *s, uint32_t wi)
         float hx, hy;
         heading(a->rw, a->rz, &hx, &hy);
         for (int k = 0; k <= ORC_SENSOR; ++k) {
-            float dx, dy;
-            ray_dir(k, hx, hy, &dx, &dy);
-            hits[k].z = wall_z(a->x, a->y, dx, dy);
-            hits[k].order = 0;
+            hits[k].z = INFINITY;
+            hits[k].order = 0xFFFFFFFFu;   /* no object */
         }
         uint32_t nf = 0;
         for (int c = 0; c < ORC_NUM_CHUNKS; ++c) {
@@ -629,6 +653,15 @@ static void world_phase_d(orc_sim *s, uint32_t wi)
         for (int32_t j = 0; j < w->n; ++j) {
             if (j == i) continue;
             raster(hits, a->x, a->y, hx, hy, w->ag[j].x, w->ag[j].y, 64u + (uint32_t)j);
+        }
+        /* resolve each ray against the walls (order 0) */
+        for (int k = 0; k <= ORC_SENSOR; ++k) {
+            float dx, dy;
+            ray_dir(k, hx, hy, &dx, &dy);
+            if (hits[k].order == 0xFFFFFFFFu || !beats_wall(a->x, a->y, dx, dy, hits[k].z)) {
+                hits[k].z = wall_z(a->x, a->y, dx, dy);
+                hits[k].order = 0;
+            }
         }
         int8_t *sem = nc->sem + (size_t)a->obs_row * ORC_SENSOR;
         uint8_t *dep = nc->depth + (size_t)a->obs_row * ORC_SENSOR;

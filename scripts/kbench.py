@@ -1,0 +1,33 @@
+#!/usr/bin/env python3
+"""Per-kernel timing of one libmbots build (A/B experiments).
+
+    MBOTS_LIB=build_var/libmbots_x.so python scripts/kbench.py [--worlds W] [--steps K]
+"""
+import argparse, json, os, sys, time
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "madrona-bots_amd"))
+import torch
+import madrona_bots as mb
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--worlds", type=int, default=65536)
+ap.add_argument("--steps", type=int, default=40)
+ap.add_argument("--warmup", type=int, default=200)
+a = ap.parse_args()
+m = mb.SimManager(0, a.worlds, 69, 32)
+m.write_synthetic_actions(1234, 0)
+for t in range(a.warmup):
+    m.step(); m.shift_observations(); m.write_synthetic_actions(1234, t + 1)
+torch.cuda.synchronize()
+m.enable_kernel_timing(True)
+s0 = m.agent_steps()
+t0 = time.perf_counter()
+for t in range(a.warmup, a.warmup + a.steps):
+    m.step(); m.shift_observations(); m.write_synthetic_actions(1234, t + 1)
+torch.cuda.synchronize()
+dt = time.perf_counter() - t0
+kt = m.kernel_times()
+out = {"lib": os.path.basename(os.environ.get("MBOTS_LIB", "default")),
+       "agent_steps_per_s": (m.agent_steps() - s0) / dt, "ms_per_step": dt / a.steps * 1e3,
+       "kernel_ms": {k: round(v[0] / v[1], 4) for k, v in kt.items() if v[1]}}
+print(json.dumps(out), flush=True)
