@@ -1,0 +1,125 @@
+#!/usr/bin/env python3
+"""Regenerates the committed fixtures under tests/golden/.
+
+1. reference_shapes.json -- facts the reference itself pins at the boundary
+   (read here from /root/reference, which is not on the GPU box):
+     * learner checkpoints (checkpoints/universe_violence/species_*/...pt,
+       loaded with torch.load(weights_only=True)): observation width 69 and
+       action width 6 (learn/env.py:19, learn/util.py:23-28);
+     * mesh extents (data/agent_render.obj, data/cube_render.obj, read as text)
+       behind the sensor's unit-circle objects.
+2. oracle_w4_a32_s69.npz / oracle_w8_a4_s7_fixed.npz -- golden vectors of the
+   CPU oracle (oracle/mbots_oracle.c, the parity checker): per-step SHA-256
+   digests of every exported column after step() and after
+   shift_observations(), and the full final tables.  The HIP path is checked
+   against these in tests/test_parity_gpu.py, the oracle itself in
+   tests/test_golden.py.
+
+    python tests/golden/make_golden.py
+"""
+import glob
+import hashlib
+import json
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+
+import pyoracle  # noqa: E402
+
+REF = "/root/reference"
+
+NAMES = ["species", "pos", "health", "surround", "reward", "action", "stats", "hidden",
+         "semantic", "depth"]
+
+FIXTURES = [
+    # name, worlds, agents, seed, steps, reward_fixed, cap
+    ("oracle_w4_a32_s69", 4, 32, 69, 16, False, 128),
+    ("oracle_w8_a4_s7_fixed", 8, 4, 7, 24, True, 16),
+]
+
+
+def digest(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()[:16]
+
+
+def table_digests(sim):
+    out = {}
+    for i, nm in enumerate(NAMES):
+        out[nm] = digest(sim.column(i))
+        out["prev_" + nm] = digest(sim.column(i, True))
+    out["species_count"] = digest(sim.species_count())
+    return out
+
+
+def run_fixture(W, A, seed, steps, reward_fixed, cap):
+    sim = pyoracle.OracleSim(W, seed, A, cap=cap, reward_fixed=reward_fixed)
+    log = [("init", sim.num_agents(), table_digests(sim))]
+    for t in range(steps):
+        sim.write_synthetic_actions(1234, t, True)
+        sim.step()
+        log.append((f"step{t}", sim.num_agents(), table_digests(sim)))
+        sim.shift_observations()
+        log.append((f"shift{t}", sim.num_agents(), table_digests(sim)))
+    return sim, log
+
+
+def save_fixture(name, W, A, seed, steps, reward_fixed, cap):
+    sim, log = run_fixture(W, A, seed, steps, reward_fixed, cap)
+    arrays = {nm: sim.column(i).copy() for i, nm in enumerate(NAMES)}
+    arrays.update({"prev_" + nm: sim.column(i, True).copy() for i, nm in enumerate(NAMES)})
+    arrays["species_count"] = sim.species_count().copy()
+    meta = {"worlds": W, "agents": A, "seed": seed, "steps": steps, "reward_fixed": reward_fixed,
+            "cap": cap, "action_seed": 1234, "write_hidden": True, "log": log}
+    np.savez_compressed(os.path.join(HERE, name + ".npz"), meta=json.dumps(meta), **arrays)
+    print(f"{name}: {sim.num_agents()} agents after {steps} steps")
+
+
+def obj_extent(path):
+    xs = []
+    with open(path) as f:
+        for line in f:
+            if line.startswith("v "):
+                xs.append([float(v) for v in line.split()[1:4]])
+    xs = np.array(xs)
+    return float(np.abs(xs).max())
+
+
+def reference_shapes():
+    import torch
+    out = {"source": "read from /root/reference by tests/golden/make_golden.py"}
+    species = {}
+    for f in sorted(glob.glob(f"{REF}/checkpoints/universe_violence/species_*/latest_model_epoch_*.pt")):
+        d = torch.load(f, weights_only=True, map_location="cpu")
+        mc = d["model_config"]
+        sd = d["model_state_dict"]
+        species[os.path.basename(os.path.dirname(f))] = {
+            "obs_dim": int(mc["layers"][0]["in_features"]),
+            "action_dim": int(mc["actor"][-1]["out_features"]),
+            "recurrent": mc["recurrent"]["type"],
+            "feature0_weight_shape": list(sd["a2c_nets.feature.0.weight"].shape),
+        }
+    out["checkpoints"] = species
+    out["obs_dim"] = sorted({v["obs_dim"] for v in species.values()})
+    out["action_dim"] = sorted({v["action_dim"] for v in species.values()})
+    out["mesh_abs_extent"] = {m: obj_extent(f"{REF}/data/{m}")
+                             for m in ("agent_render.obj", "cube_render.obj")}
+    return out
+
+
+def main():
+    pyoracle.build()
+    if os.path.isdir(REF):
+        with open(os.path.join(HERE, "reference_shapes.json"), "w") as f:
+            json.dump(reference_shapes(), f, indent=1, sort_keys=True)
+        print("reference_shapes.json written")
+    for fx in FIXTURES:
+        save_fixture(*fx)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,51 @@
+"""The rollout harness (madrona-bots_amd/harness/rollout.py, the learn/env.py
+call sequence): BASELINE config 1 -- 64 worlds on the CPU through the oracle
+adapter -- and the same loop on the GPU product."""
+import os
+import sys
+
+import pytest
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "madrona-bots_amd", "harness"))
+
+import rollout  # noqa: E402
+from oracle_adapter import OracleSimManager  # noqa: E402
+
+
+@pytest.mark.parametrize("per_species", [False, True])
+def test_config1_cpu_rollout(per_species):
+    sim = OracleSimManager(0, 64, 69, 32)
+    st = rollout.random_rollout(sim, 8, shift_per_species=per_species)
+    assert st["steps"] == 8 and st["agent_steps"] >= 64 * 32 * 8
+    offs = rollout.species_offsets(sim)
+    assert offs[0][0] == 0 and all(a[1] == b[0] for a, b in zip(offs, offs[1:]))
+    obs = rollout.construct_obs(sim, *offs[2])
+    assert obs.shape[1] == rollout.OBS_DIM == 69 and obs.dtype == torch.float32
+
+
+def test_per_species_shift_overwrites_prev_actions():
+    # shifting inside the species loop makes PrevAction of species
+    # 1..3 equal their *new* actions; only species 4 keeps its true previous ones
+    sim = OracleSimManager(0, 8, 69, 32)
+    rollout.random_rollout(sim, 3, shift_per_species=True)
+    offs = rollout.species_offsets(sim)
+    act = sim.action_tensor(False).to_torch()
+    pact = sim.action_tensor(True).to_torch()
+    for s, e in offs[:3]:
+        assert torch.equal(pact[s:e], act[s:e])
+    s, e = offs[3]
+    assert pact[s:e].sum() == e - s        # one-hot previous actions of species 4
+
+
+@pytest.mark.gpu
+def test_gpu_rollout():
+    import madrona_bots as mb
+    dev = torch.device("cuda", 0)
+    sim = mb.SimManager(0, 256, 69, 32)
+    st = rollout.random_rollout(sim, 6, device=dev)
+    assert st["steps"] == 6
+    offs = rollout.species_offsets(sim)
+    obs = rollout.construct_obs(sim, *offs[0], prev=True)
+    assert obs.shape[1] == 69 and obs.device.type == "cuda"

@@ -1,0 +1,225 @@
+"""CPU: known-answer tests of the oracle (oracle/mbots_oracle.c), hand-derived
+from the cited reference formulas, plus independent numpy restatements of the
+small systems.  No GPU needed."""
+import numpy as np
+import pytest
+
+import pyoracle as po
+
+
+def f32(x):
+    return np.float32(x)
+
+
+# ---------------------------------------------------------------------------
+# RNG: Threefry-2x32-20 known-answer vectors published with Random123
+# (kat_vectors: "threefry2x32 20 <ctr0> <ctr1> <key0> <key1> <out0> <out1>")
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("ctr,key,out", [
+    ((0x00000000, 0x00000000), (0x00000000, 0x00000000), (0x6b200159, 0x99ba4efe)),
+    ((0xffffffff, 0xffffffff), (0xffffffff, 0xffffffff), (0x1cb996fc, 0xbb002be7)),
+    ((0x243f6a88, 0x85a308d3), (0x13198a2e, 0x03707344), (0xc4923a9c, 0x483df7a0)),
+])
+def test_threefry_kat(ctr, key, out):
+    assert po.threefry2x32(key, ctr) == out
+
+
+def test_samplers():
+    L = po.lib()
+    assert L.orc_sample_uniform(0) == 0.0
+    assert L.orc_sample_uniform(0xFFFFFFFF) == f32(16777215 / 16777216)
+    for bits in (0, 1, 0x7FFFFFFF, 0x80000000, 0xFFFFFFFF, 12345678):
+        v = L.orc_sample_i32(bits, 0, 10)
+        assert 0 <= v < 10 and v == (bits * 10) >> 32
+        assert 1 <= L.orc_sample_i32(bits, 1, 3) < 3
+
+
+def _rows_by_species(sim):
+    """A=4, one agent per species, no deaths: row r holds species r+1."""
+    sp = sim.column(po.COL_SPECIES).ravel()
+    assert list(sp) == [1, 2, 3, 4]
+
+
+# ---------------------------------------------------------------------------
+# actionSystem (sim.cpp:419-502)
+# ---------------------------------------------------------------------------
+def test_forward_step_moves_plus_one_x():
+    sim = po.OracleSim(1, 69, 4, cap=16)
+    _rows_by_species(sim)
+    p0 = sim.column(po.COL_POS).copy()
+    act = sim.column(po.COL_ACTION)
+    act[:] = 0
+    act[:, 0] = 1                       # forward
+    sim.step()
+    _rows_by_species(sim)
+    p1 = sim.column(po.COL_POS)
+    # identity rotation: view_dir = (1 - 2*0, 2*0*1) = (1, 0) exactly
+    exp_x = np.minimum(f32(127.0), np.maximum(f32(0.0), p0[:, 0] + f32(1.0)))
+    assert np.array_equal(p1[:, 0], exp_x)
+    assert np.array_equal(p1[:, 1], p0[:, 1])
+
+
+def test_rotate_left_ten_times_then_forward():
+    sim = po.OracleSim(1, 3, 4, cap=16)
+    act = sim.column(po.COL_ACTION)
+    for _ in range(10):
+        act = sim.column(po.COL_ACTION)
+        act[:] = 0
+        act[:, 2] = 1                   # rotateLeft: rot *= angleAxis(0.1, z)
+        sim.step()
+    p0 = sim.column(po.COL_POS).copy()
+    act = sim.column(po.COL_ACTION)
+    act[:] = 0
+    act[:, 0] = 1
+    sim.step()
+    d = sim.column(po.COL_POS) - p0
+    want = np.array([np.cos(1.0), np.sin(1.0)])
+    for k in range(4):
+        x, y = p0[k]
+        if 2 < x < 125 and 2 < y < 93:          # not clamped by the walls
+            assert np.allclose(d[k], want, atol=1e-5), (d[k], want)
+
+
+# ---------------------------------------------------------------------------
+# speciesInfoSync (sim.cpp:791-838) + rewardSystem setting 8 (sim.cpp:942-956)
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("fixed", [False, True])
+def test_reward_no_events(fixed):
+    sim = po.OracleSim(1, 69, 4, cap=16, reward_fixed=fixed)
+    act = sim.column(po.COL_ACTION)
+    act[:] = 0
+    sim.step()
+    _rows_by_species(sim)
+    assert not sim.column(po.COL_STATS).any()
+    assert list(sim.column(po.COL_HEALTH).ravel()) == [100] * 4
+    # rewards[i] = count/A + avg/100 - 2 = 1/4 + 1 - 2 = -0.75
+    sr = f32(f32(f32(1.0) / f32(4.0)) + f32(f32(100.0) / f32(100.0))) - f32(2.0)
+    r_own = f32(f32(sr + f32(f32(100.0) / f32(100.0))) - f32(0.5))
+    rew = sim.column(po.COL_REWARD).ravel()
+    if fixed:
+        assert list(rew) == [r_own] * 4
+    else:
+        # faithful rewards[speciesID]: species 1..3 read rewards[1..3] (= -0.75),
+        # species 4 reads past the array -> 0 for the table's last world (B.3)
+        r4 = f32(f32(f32(0.0) + f32(1.0)) - f32(0.5))
+        assert list(rew) == [r_own, r_own, r_own, r4]
+
+
+def test_respawn_refills_species():
+    # A = 4: any species that drops below A/4 = 1 is respawned in the same step
+    sim = po.OracleSim(16, 5, 4, cap=16)
+    for t in range(40):
+        sim.write_synthetic_actions(99, t)
+        sim.step()
+        assert (sim.species_count() >= 1).all()
+
+
+# ---------------------------------------------------------------------------
+# updateSurroundingObservation (sim.cpp:583-654): numpy float32 restatement
+# ---------------------------------------------------------------------------
+def _chunk_index(cx, cy):
+    x, y = int(cx), int(cy)
+    if x < 0 or y < 0 or x >= 8 or y >= 6:
+        return -1
+    return x + y * 8
+
+
+def test_surrounding_matches_numpy_restatement():
+    W = 4
+    sim = po.OracleSim(W, 69, 32, cap=128)
+    p0 = sim.column(po.COL_POS).copy()
+    act = sim.column(po.COL_ACTION)
+    act[:] = 0          # no actions: the only motion is the clamp to [0, Lx-1] x [0, Ly-1]
+    sim.step()
+    assert sim.num_agents() == W * 32        # nobody born or died: rows are stable
+    pos = sim.column(po.COL_POS)
+    sur = sim.column(po.COL_SURROUND)
+    # clamp (sim.cpp:485-486) and the speed heuristic (u32)(2 |dpos|) (sim.cpp:488-501)
+    assert np.array_equal(pos[:, 0], np.minimum(f32(127), np.maximum(f32(0), p0[:, 0])))
+    assert np.array_equal(pos[:, 1], np.minimum(f32(95), np.maximum(f32(0), p0[:, 1])))
+    d = pos - p0
+    speed = (np.sqrt(d[:, 0] * d[:, 0] + d[:, 1] * d[:, 1]) * f32(2)).astype(np.uint32)
+    # export rows are ordered (species, world, slot): rebuild per-world row lists
+    sc = sim.species_count()
+    row = 0
+    rows_of = {w: [] for w in range(W)}
+    for s in range(4):
+        for w in range(W):
+            rows_of[w] += list(range(row, row + sc[w, s]))
+            row += sc[w, s]
+    for w in range(W):
+        rr = rows_of[w]
+        n_ag = np.zeros(48, np.uint32)
+        t_sp = np.zeros(48, np.uint32)
+        for r in rr:
+            c = _chunk_index(np.floor(pos[r, 0] / f32(16)), np.floor(pos[r, 1] / f32(16)))
+            n_ag[c] += 1
+            t_sp[c] += speed[r]
+        for r in rr:
+            cpx = pos[r, 0] - f32(8.0)
+            cpy = pos[r, 1] - f32(8.0)
+            chx, chy = cpx / f32(16), cpy / f32(16)
+            x0, y0, x1, y1 = np.floor(chx), np.floor(chy), np.ceil(chx), np.ceil(chy)
+            idx = [_chunk_index(x0, y0), _chunk_index(x1, y0), _chunk_index(x0, y1),
+                   _chunk_index(x1, y1)]
+            xi, yi = chx - x0, chy - y0
+            for col, cnt in ((0, n_ag), (1, t_sp)):
+                n = [f32(cnt[i]) if i >= 0 else f32(0) for i in idx]
+                nx0 = xi * n[1] + (f32(1) - xi) * n[0]
+                nx1 = xi * n[3] + (f32(1) - xi) * n[2]
+                want = yi * nx1 + (f32(1) - yi) * nx0
+                assert sur[r, col] == want, (w, r, col, sur[r, col], want)
+
+
+def test_surround_at_chunk_centroid_is_that_count():
+    # at a chunk centroid (8 + 16 i, 8 + 16 j) the interpolants are 0 and the
+    # presence heuristic is exactly that chunk's agent count
+    chx = (f32(8 + 16 * 3) - f32(8)) / f32(16)
+    assert chx - np.floor(chx) == 0.0
+
+
+# ---------------------------------------------------------------------------
+# Export invariants and shift_observations (sim.cpp:1002-1048)
+# ---------------------------------------------------------------------------
+def test_export_invariants_and_shift():
+    sim = po.OracleSim(32, 11, 32, cap=128)
+    for t in range(30):
+        sim.write_synthetic_actions(1234, t, True)
+        sim.step()
+        N = sim.num_agents()
+        sc = sim.species_count()
+        assert sc.sum() == N
+        sp = sim.column(po.COL_SPECIES).ravel()
+        assert (np.diff(sp) >= 0).all()             # species-major rows
+        assert list(np.bincount(sp, minlength=5)[1:]) == list(sc.sum(0))
+        assert (sim.column(po.COL_HEALTH) > 0).all()
+        sem = sim.column(po.COL_SEMANTIC)
+        assert sem.min() >= 1 and sem.max() <= 6
+        sim.shift_observations()
+        for c in (po.COL_SPECIES, po.COL_POS, po.COL_HEALTH, po.COL_SURROUND, po.COL_REWARD,
+                  po.COL_ACTION, po.COL_HIDDEN):
+            assert np.array_equal(sim.column(c), sim.column(c, True))
+        st, pst = sim.column(po.COL_STATS), sim.column(po.COL_STATS, True)
+        assert np.array_equal(pst[:, [0, 2, 3]], st[:, [0, 2, 3]])
+        assert np.array_equal(pst[:, 1], st[:, 0])  # hitEnemy <- hitFriendly (sim.cpp:1034)
+    assert sim.overflow() == 0
+
+
+def test_prev_sensor_is_last_steps_sensor():
+    sim = po.OracleSim(1, 69, 4, cap=16)
+    act = sim.column(po.COL_ACTION)
+    act[:] = 0
+    sim.step()
+    sem0 = sim.column(po.COL_SEMANTIC).copy()
+    act = sim.column(po.COL_ACTION)
+    act[:] = 0
+    act[:, 2] = 1
+    sim.step()
+    _rows_by_species(sim)
+    assert np.array_equal(sim.column(po.COL_SEMANTIC, True), sem0)
+
+
+def test_health_export_is_int_bits():
+    # health_tensor views int32 health as float32 (types.hpp:119-124, mgr.cpp:397-414)
+    h = np.array([100], np.int32).view(np.float32)[0]
+    assert h == np.float32(1.4e-43)
