@@ -29,11 +29,25 @@ ACTION_SEED = 1234
 AGENTS_PER_WORLD = 32       # learn/env.py:15
 
 
-def algorithmic_bytes(kernel, n_agents, n_worlds):
-    """B_step = 552 N + 1952 W, split per kernel."""
-    if kernel == "shift":
-        return 264.0 * n_agents
-    return 288.0 * n_agents + 1952.0 * n_worlds
+def algorithmic_bytes(n_agents, n_worlds):
+    """B_step = 552 N + 1952 W bytes per step (step + shift)."""
+    return 552.0 * n_agents + 1952.0 * n_worlds
+
+
+def load_traffic(worlds):
+    """HBM bytes per step from the committed rocprofv3 PMC summary
+    (profiles/*_traffic.json, scripts/traffic.py: 2 x FETCH_SIZE + WRITE_SIZE per
+    MI355X_MICROARCH.md 'HBM'), or None."""
+    import glob
+    best = None
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_traffic.json"))):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        if d.get("worlds") == worlds:
+            best = (os.path.relpath(f, ROOT), d)
+    return best
 
 
 def cpu_baseline(worlds_sample, target_s):
@@ -100,18 +114,28 @@ def main():
     steps_before = mgr.agent_steps()
     if not args.no_kernel_timing:
         mgr.enable_kernel_timing(True)
+    # device span of step()+shift_observations() on the launch stream (torch's
+    # current stream is the stream libmbots launches on; step() joins its
+    # internal aux stream back into it)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(args.steps)]
 
     if distributed:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for t in range(args.warmup, args.warmup + args.steps):
-        one_step(t)
+    for k, t in enumerate(range(args.warmup, args.warmup + args.steps)):
+        ev[k][0].record()
+        mgr.step()
+        mgr.shift_observations()
+        ev[k][1].record()
+        mgr.write_synthetic_actions(ACTION_SEED, t + 1)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     if distributed:
         dist.barrier()
     elapsed = t1 - t0
+    span_ms = sum(a.elapsed_time(b) for a, b in ev) / args.steps
 
     agent_steps = mgr.agent_steps() - steps_before
     ktimes = mgr.kernel_times() if not args.no_kernel_timing else {}
@@ -149,20 +173,22 @@ def main():
                        "world_steps_per_s": W * world_size * args.steps / elapsed,
                        "parallelism": f"world-shard x{world_size}, no collective"},
         }
+        nb = algorithmic_bytes(mean_agents, W)
+        achieved = nb / (span_ms * 1e-3) / 1e9
+        roof = {"bound": "hbm", "kernel": "world step: step()+shift_observations() "
+                "(K1 world_step, K2 scan, K3a export_rows, K4 move || K3b sensor, K5 shift)",
+                "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                "algorithmic_bytes_per_launch": nb, "avg_launch_ms": span_ms,
+                "timing": "HIP events on the launch stream around each step()+shift()"}
+        tr = load_traffic(W)
+        if tr:
+            roof["traffic"] = tr[1]["bytes_per_step"]
+            roof["traffic_source"] = tr[0]
+        out["roofline"] = roof
         if ktimes:
             per = {k: (ms / n if n else 0.0) for k, (ms, n) in ktimes.items()}
-            out["kernel_ms"] = {k: round(v, 5) for k, v in per.items()}
-            step_ms = sum(per[k] for k in ("world_step", "scan", "export", "sensor"))
-            shift_ms = per["shift"]
-            cand = {"step": step_ms, "shift": shift_ms}
-            dom = max(cand, key=cand.get)
-            nb = algorithmic_bytes(dom, mean_agents, W)
-            achieved = nb / (cand[dom] * 1e-3) / 1e9
-            out["roofline"] = {"bound": "hbm", "kernel": dom, "achieved": achieved,
-                               "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                               "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                               "algorithmic_bytes_per_launch": nb,
-                               "avg_launch_ms": cand[dom]}
+            out["kernel_ms"] = {k: round(v, 5) for k, v in per.items() if v}
         if not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args.cpu_worlds, args.cpu_seconds)
         print(json.dumps(out), flush=True)
