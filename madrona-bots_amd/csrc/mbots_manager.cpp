@@ -73,6 +73,7 @@ struct mbots_handle {
     hipEvent_t ev_totals = nullptr;
     hipStream_t aux = nullptr;        // internal stream: K4 move next to the K3b sensor
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    bool sensor_pending = false;      // K3b still running on aux (ev_join)
     hipStream_t last_stream = nullptr;
     bool timing = false;
     std::vector<TimedPair> pending;
@@ -177,6 +178,13 @@ size_t layout(mbots_handle *h, Arena &a)
 }
 
 hipStream_t as_stream(void *s) { return reinterpret_cast<hipStream_t>(s); }
+
+// make the caller's stream (the one step() ran on) wait for the sensor rows
+int wait_sensor(mbots_handle *h)
+{
+    if (h->sensor_pending) HIP_TRY(hipStreamWaitEvent(h->last_stream, h->ev_join, 0));
+    return MBOTS_OK;
+}
 
 int sync_totals(mbots_handle *h)
 {
@@ -305,6 +313,9 @@ int mbots_step(mbots_handle *h, void *stream)
     const mbots::ObsTable &nxt = h->T[h->tb ^ 1];
     int rc;
     const int par = h->parity;
+    // the previous step's sensor (aux) wrote the finder slots K1 reads and the
+    // semantic rows K4 moves into the prev-sensor column
+    if (h->sensor_pending) HIP_TRY(hipStreamWaitEvent(st, h->ev_join, 0));
     if ((rc = timed(h, MBOTS_TK_WORLD_STEP, st,
                     [&] { return mbots::launch_world_step(h->S, cur, par, st); })))
         return rc;
@@ -317,16 +328,20 @@ int mbots_step(mbots_handle *h, void *stream)
         return rc;
     if ((rc = timed(h, MBOTS_TK_SENSOR, st, [&] { return mbots::launch_sensor(h->S, nxt, st); })))
         return rc;
+    h->sensor_pending = false;
 #else
-    // fork: K4 move (HBM stream) on the aux stream || K3b sensor (VALU) on st
+    // fork: K3b sensor (VALU-bound) on the aux stream; the caller's stream goes
+    // on with K4 move and whatever follows (shift_observations, the learner's
+    // action writes) -- none of it reads the sensor output.  The next step and
+    // the semantic/depth accessors wait for ev_join.
     HIP_TRY(hipEventRecord(h->ev_fork, st));
     HIP_TRY(hipStreamWaitEvent(h->aux, h->ev_fork, 0));
-    if ((rc = timed(h, MBOTS_TK_MOVE, h->aux, [&] { return mbots::launch_move(h->S, cur, nxt, h->aux); })))
+    if ((rc = timed(h, MBOTS_TK_SENSOR, h->aux, [&] { return mbots::launch_sensor(h->S, nxt, h->aux); })))
         return rc;
     HIP_TRY(hipEventRecord(h->ev_join, h->aux));
-    if ((rc = timed(h, MBOTS_TK_SENSOR, st, [&] { return mbots::launch_sensor(h->S, nxt, st); })))
+    h->sensor_pending = true;
+    if ((rc = timed(h, MBOTS_TK_MOVE, st, [&] { return mbots::launch_move(h->S, cur, nxt, st); })))
         return rc;
-    HIP_TRY(hipStreamWaitEvent(st, h->ev_join, 0));
 #endif
     h->parity ^= 1;
     h->tb ^= 1;
@@ -379,9 +394,12 @@ int mbots_export(mbots_handle *h, int32_t id, mbots_tensor *out)
     case MBOTS_EXPORT_PREV_HEALTH: p = t.phealth; dt = MBOTS_DTYPE_FLOAT32; break;
     case MBOTS_EXPORT_SURROUNDING: p = t.sur; dt = MBOTS_DTYPE_FLOAT32; cols = 2; break;
     case MBOTS_EXPORT_PREV_SURROUNDING: p = t.psur; dt = MBOTS_DTYPE_FLOAT32; cols = 2; break;
-    case MBOTS_EXPORT_SENSOR_SEMANTIC: p = t.sem; dt = MBOTS_DTYPE_INT8; cols = kSensor; break;
+    case MBOTS_EXPORT_SENSOR_SEMANTIC:
+        if ((rc = wait_sensor(h))) return rc;
+        p = t.sem; dt = MBOTS_DTYPE_INT8; cols = kSensor; break;
     // SensorDepth exports the semantic buffer (sim.cpp:102-104, B.1) unless fixed
     case MBOTS_EXPORT_SENSOR_DEPTH:
+        if ((rc = wait_sensor(h))) return rc;
         p = fixd ? (void *)t.depth : (void *)t.sem; dt = MBOTS_DTYPE_UINT8; cols = kSensor; break;
     case MBOTS_EXPORT_PREV_SENSOR_SEMANTIC: p = t.psem; dt = MBOTS_DTYPE_INT8; cols = kSensor; break;
     case MBOTS_EXPORT_PREV_SENSOR_DEPTH:
@@ -415,8 +433,9 @@ int mbots_set_action(mbots_handle *h, uint32_t row, const int32_t action[6])
     int rc = mbots_num_agents(h, &N);
     if (rc) return rc;
     if (row >= N) return fail(MBOTS_E_RANGE, "agent row out of range");
-    HIP_TRY(hipMemcpy(h->T[h->tb].action + (size_t)row * 6, action, 6 * sizeof(int32_t),
-                      hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpyAsync(h->T[h->tb].action + (size_t)row * 6, action, 6 * sizeof(int32_t),
+                           hipMemcpyHostToDevice, h->last_stream));
+    HIP_TRY(hipStreamSynchronize(h->last_stream));
     return MBOTS_OK;
 }
 
