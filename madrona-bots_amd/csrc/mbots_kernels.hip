@@ -618,13 +618,15 @@ __global__ __launch_bounds__(256) void move_kernel(const uint32_t *totals, const
 // the wall (z * d < X - o per axis), else the wall (order 0).
 //
 // One wave per world, agents in chunks of kKeyAgents; per chunk:
-//  pairs  every (agent, object) pair, one per lane, branch-light: approximate
-//         roots of q bound the candidate pixels; the exact predicate runs on
-//         (at most) 3 candidates + the finder and ds_min_u32's the 32-bit key
-//         (z with its low 8 mantissa bits replaced by the object order);
-//         pairs near the agent or covering more pixels go to a wide list that
-//         the whole wave evaluates on all 33 rays;
-//  output per (agent, ray): key vs wall -> semantic / depth bytes; finder.
+//  P1  all (agent, object) pairs, one per lane: f, l and the wedge test
+//      |l| <= |f| + sqrt(2) (necessary for any pixel, |u| < 1); survivors and
+//      their (f, l) are ballot-compacted into a queue;
+//  P2  per survivor: approximate roots of q bound its candidate pixels; <= 2
+//      pixels + the finder run the exact predicate inline and ds_min_u32 the
+//      32-bit key (z with its low 8 mantissa bits replaced by the object
+//      order); nearer / wider pairs go to a wide list;
+//  W   wide pairs: two per wave, one lane per ray;
+//  out per (agent, ray): key vs wall -> semantic / depth bytes; finder slot.
 // The exact predicate and depths use the same float expressions as
 // oracle/mbots_oracle.c; culling only skips rays it proves cannot pass.
 // ---------------------------------------------------------------------------
@@ -635,7 +637,8 @@ __global__ __launch_bounds__(256) void move_kernel(const uint32_t *totals, const
 #define MB_ABL 0                              // timing ablations: 1 no sensor work, 8 no output
 #endif
 constexpr int kKeyAgents = MB_KEY_AGENTS;     // agents per chunk (key rows)
-constexpr int kWideCap = 128;                 // wide-pair list (flushed above 64)
+constexpr int kQueueCap = 128;                // P1 survivors (flushed at >= 64)
+constexpr int kWideCap = 64;                  // wide pairs of one survivor batch
 constexpr int kMaxFood = kFoodCap + 2;        // live packages == currentNumFood <= 30
 constexpr float kWedge = 1.41421356f + 0.05f; // |l| <= |f| + sqrt(2): necessary for |u| < 1
 constexpr float kUEps = 2e-3f;                // root-interval margin in u
@@ -644,12 +647,15 @@ constexpr uint32_t kOrderAgent = 64u;
 constexpr uint32_t kNoKey = 0xFFFFFFFFu;
 
 struct SensorLDS {
-    float ox[kMaxFood + kMaxCap], oy[kMaxFood + kMaxCap];   // food then agents
-    float hx[kMaxCap], hy[kMaxCap];
-    int32_t sp[kMaxCap];
-    int32_t row[kMaxCap];                                   // new export row per slot
+    float2 obj[kMaxFood + kMaxCap];           // positions: food, then agents
+    float2 hd[kMaxCap];                       // agent headings
+    int8_t sp[kMaxCap];
+    int32_t row[kMaxCap];                     // new export row per slot
     uint32_t key[kKeyAgents * kRays];
-    uint32_t wide[kWideCap];
+    uint32_t qcode[kQueueCap];                // P1 survivors: code, f, l
+    float qf[kQueueCap], ql[kQueueCap];
+    uint32_t wcode[kWideCap];                 // wide pairs: code, f, l
+    float wf[kWideCap], wl[kWideCap];
     float u[kSensor];
 };
 
@@ -674,9 +680,11 @@ __device__ __forceinline__ uint32_t zkey(float z, uint32_t order)
     return (__float_as_uint(z) & ~0xFFu) | order;
 }
 
+// predicates below use non-short-circuit & | so they compile to VALU selects,
+// not exec-mask branches; the float operations are the oracle's
 __device__ __forceinline__ bool inside_arena(float ox, float oy)
 {
-    return ox >= kInLo && ox <= kInHiX && oy >= kInLo && oy <= kInHiY;
+    return (ox >= kInLo) & (ox <= kInHiX) & (oy >= kInLo) & (oy <= kInHiY);
 }
 
 // wall depth of a ray: exit from the inner rectangle; 0 inside a wall box
@@ -695,40 +703,135 @@ __device__ __forceinline__ float wall_z(float ox, float oy, float dx, float dy)
 // object at view depth z hides the wall iff z * d < (X - o) per axis
 __device__ __forceinline__ bool beats_wall(float ox, float oy, float dx, float dy, float z)
 {
-    const bool bx = dx > 0.0f ? (z * dx < kInHiX - ox) : (dx < 0.0f ? (z * dx > kInLo - ox) : true);
-    const bool by = dy > 0.0f ? (z * dy < kInHiY - oy) : (dy < 0.0f ? (z * dy > kInLo - oy) : true);
-    return inside_arena(ox, oy) && bx && by;
+    const float zx = z * dx, zy = z * dy;
+    const bool bx = ((dx > 0.0f) & (zx < kInHiX - ox)) | ((dx < 0.0f) & (zx > kInLo - ox)) |
+                    (dx == 0.0f);
+    const bool by = ((dy > 0.0f) & (zy < kInHiY - oy)) | ((dy < 0.0f) & (zy > kInLo - oy)) |
+                    (dy == 0.0f);
+    return inside_arena(ox, oy) & bx & by;
 }
 
-// the whole wave evaluates one wide pair (agent ic of the chunk, object j) on
-// rays 0..32 (lane = ray)
-__device__ __forceinline__ void wide_pair(SensorLDS &L, int a0, int nf, uint32_t code)
+// (f, l) of object j in agent i's frame; order of the object
+__device__ __forceinline__ void pair_fl(const SensorLDS &L, int nf, int i, int j, float &f,
+                                        float &l, uint32_t &order)
 {
-    const int lane = (int)__lane_id();
-    const int ic = (int)(code & 0xFFu), j = (int)(code >> 8);
-    const int i = a0 + ic;
-    const float hx = L.hx[i], hy = L.hy[i];
-    const float vx = L.ox[j] - L.ox[nf + i], vy = L.oy[j] - L.oy[nf + i];
-    const float f = vx * hx + vy * hy;
-    const float l = vx * hy - vy * hx;
-    const uint32_t order = j < nf ? kOrderFood + (uint32_t)j : kOrderAgent + (uint32_t)(j - nf);
-    const float r2 = f * f + l * l;
+    const float2 a = L.obj[nf + i];
+    const float2 h = L.hd[i];
+    const float2 p = L.obj[j];
+    order = j < nf ? kOrderFood + (uint32_t)j : kOrderAgent + (uint32_t)(j - nf);
+    const float vx = p.x - a.x, vy = p.y - a.y;
+    f = vx * h.x + vy * h.y;   // along the heading
+    l = vx * h.y - vy * h.x;   // along r = (hy, -hx)
+}
+
+__device__ __forceinline__ uint32_t order_of(int nf, int j)
+{
+    return j < nf ? kOrderFood + (uint32_t)j : kOrderAgent + (uint32_t)(j - nf);
+}
+
+// exact predicate of (f, l) on pixel ray k < 32 with offset u; key or kNoKey
+__device__ __forceinline__ uint32_t pixel_key(float f, float l, float u, bool fwdk, uint32_t order)
+{
     const float A = f * f - 1.0f, B2 = 2.0f * (l * f), C = l * l - 1.0f;
-    bool hit;
-    float z;
-    if (lane < kSensor) {
-        const float u = L.u[lane];
-        const float q = (A * u - B2) * u + C;
-        const float p = f + u * l;
-        const bool fwdk = lane < 24;
-        hit = q <= 0.0f && (fwdk ? p > 0.0f : p < 0.0f);
-        z = zq(max0(fwdk ? f - 1.0f : -f - 1.0f));
-    } else {
-        hit = C <= 0.0f && f > 0.0f;
-        z = zq(max0(f - 1.0f));
+    const float q = (A * u - B2) * u + C;
+    const float p = f + u * l;
+    const bool hit = (q <= 0.0f) & ((fwdk & (p > 0.0f)) | (!fwdk & (p < 0.0f)));
+    const float z = zq(max0(fwdk ? f - 1.0f : -f - 1.0f));
+    const bool near = f * f + l * l <= 1.0f;
+    const uint32_t key = zkey(near ? 0.0f : z, order);
+    return (hit | near) ? key : kNoKey;
+}
+
+// the finder ray (u = 0)
+__device__ __forceinline__ uint32_t finder_key(float f, float l, uint32_t order)
+{
+    const float C = l * l - 1.0f;
+    const bool hit = (C <= 0.0f) & (f > 0.0f);
+    const bool near = f * f + l * l <= 1.0f;
+    const uint32_t key = zkey(near ? 0.0f : zq(max0(f - 1.0f)), order);
+    return (hit | near) ? key : kNoKey;
+}
+
+// W: wide pairs [0, cnt), two per wave (32 lanes each: rays 0..31, lane 0 of
+// each half also takes the finder ray)
+__device__ __forceinline__ void run_wide(SensorLDS &L, int nf, int cnt)
+{
+    if (MB_ABL & 32) return;
+    const int lane = (int)__lane_id();
+    for (int e0 = 0; e0 < cnt; e0 += 2) {
+        const int e = e0 + (lane >> 5);
+        if (e < cnt) {
+            const uint32_t code = L.wcode[e];
+            const float f = L.wf[e], l = L.wl[e];
+            const int ic = (int)(code & 0x1Fu), j = (int)(code >> 11);
+            const uint32_t order = order_of(nf, j);
+            uint32_t *kr = L.key + ic * kRays;
+            const int k = lane & 31;
+            const uint32_t kv = pixel_key(f, l, L.u[k], k < 24, order);
+            if (kv != kNoKey) atomicMin(&kr[k], kv);
+            const uint32_t kf = finder_key(f, l, order);
+            if ((k == 0) & (kf != kNoKey)) atomicMin(&kr[kSensor], kf);
+        }
     }
-    if (r2 <= 1.0f) { hit = true; z = 0.0f; }
-    if (lane <= kSensor && hit) atomicMin(&L.key[ic * kRays + lane], zkey(z, order));
+}
+
+// P2: survivors [q0, q0 + cnt): approximate roots bound the candidate pixels;
+// <= 2 pixels + the finder are tested inline, wider pairs go to the wide list
+__device__ __forceinline__ void run_survivors(SensorLDS &L, int nf, int q0, int cnt)
+{
+    if (MB_ABL & 16) return;
+    const int lane = (int)__lane_id();
+    bool wide = false;
+    uint32_t code = 0;
+    float f = 0.0f, l = 0.0f;
+    if (lane < cnt) {
+        code = L.qcode[q0 + lane];
+        f = L.qf[q0 + lane];
+        l = L.ql[q0 + lane];
+        const int ic = (int)(code & 0x1Fu), j = (int)(code >> 11);
+        const uint32_t order = order_of(nf, j);
+        const float r2 = f * f + l * l;
+        if (r2 <= 1.0f || fabsf(f) <= 1.5f) {
+            wide = true;
+        } else {
+            const bool fwd = f > 0.0f;
+            const float sq = __builtin_amdgcn_sqrtf(r2 - 1.0f);
+            const float ia = __builtin_amdgcn_rcpf(f * f - 1.0f);
+            const float u1 = (l * f - sq) * ia - kUEps, u2 = (l * f + sq) * ia + kUEps;
+            const float sc = fwd ? 12.0f : 4.0f, kmax = fwd ? 23.0f : 7.0f;
+            const float lo = fmaxf((u1 + 1.0f) * sc - 0.5f, -1.0f);
+            const float hi = fminf((u2 + 1.0f) * sc - 0.5f, kmax + 1.0f);
+            int k0 = max((int)ceilf(lo), 0);
+            const int k1 = min((int)floorf(hi), (int)kmax);
+            const int c = k1 - k0 + 1;
+            k0 += fwd ? 0 : 24;
+            if (c > 2) {
+                wide = true;
+            } else if (!(MB_ABL & 32)) {
+                uint32_t *kr = L.key + ic * kRays;
+                const float ua = L.u[k0 & 31], ub = L.u[(k0 + 1) & 31];
+                const uint32_t ka = pixel_key(f, l, ua, fwd, order);
+                const uint32_t kb = pixel_key(f, l, ub, fwd, order);
+                const uint32_t kf = finder_key(f, l, order);
+                if ((c > 0) & (ka != kNoKey)) atomicMin(&kr[k0], ka);
+                if ((c > 1) & (kb != kNoKey)) atomicMin(&kr[k0 + 1], kb);
+                if (fwd & (u1 <= 0.0f) & (u2 >= 0.0f) & (kf != kNoKey)) atomicMin(&kr[kSensor], kf);
+            }
+        }
+    }
+    const uint64_t wm = ballot64(wide);
+    if (wide) {
+        const int s = (int)rank_below(wm);
+        L.wcode[s] = code;
+        L.wf[s] = f;
+        L.wl[s] = l;
+    }
+    const int nw = __popcll(wm);
+    if (nw > 0) {
+        wave_sync();
+        run_wide(L, nf, nw);
+        wave_sync();
+    }
 }
 
 __global__ __launch_bounds__(256) void sensor_kernel(SimState S, ObsTable nxt)
@@ -765,91 +868,69 @@ __global__ __launch_bounds__(256) void sensor_kernel(SimState S, ObsTable nxt)
         for (int k = 0; k < kMaxPkg; ++k) {
             if ((live >> k) & 1u) {
                 const uint32_t xy = (uint32_t)(rec >> (8 * k)) & 0xFFu;
-                if (s < kMaxFood) {   // live packages == currentNumFood <= 30
-                    L.ox[s] = (float)(xy & 15u) + bx;
-                    L.oy[s] = (float)(xy >> 4) + by;
-                }
+                if (s < kMaxFood)   // live packages == currentNumFood <= 30
+                    L.obj[s] = make_float2((float)(xy & 15u) + bx, (float)(xy >> 4) + by);
                 ++s;
             }
         }
         nf = min(tot, kMaxFood);
     }
+    // ---- agents -> objects [nf, nf + n) ----
     for (int i = lane; i < n; i += 64) {
         float hx, hy;
         heading(S.rw[base + i], S.rz[base + i], hx, hy);
-        L.ox[nf + i] = S.x[base + i];
-        L.oy[nf + i] = S.y[base + i];
-        L.sp[i] = S.species[base + i];
-        L.hx[i] = hx;
-        L.hy[i] = hy;
+        const float x = S.x[base + i], y = S.y[base + i];
+        L.obj[nf + i] = make_float2(x, y);
+        L.hd[i] = make_float2(hx, hy);
+        L.sp[i] = (int8_t)S.species[base + i];
         L.row[i] = S.obsrow[base + i];
     }
     if (MB_ABL & 1) return;
     const int nobj = nf + n;
-    const float inv_nobj = 1.0f / (float)nobj;
     wave_sync();
 
     for (int a0 = 0; a0 < n; a0 += kKeyAgents) {
         const int nc = min(kKeyAgents, n - a0);
         for (int q = lane; q < nc * kRays; q += 64) L.key[q] = kNoKey;
         wave_sync();
-        // ---- pairs ----
+        // ---- P1: wedge pre-cull of the chunk's (agent, object) pairs ----
+        int nq = 0;
+        int ic = 0, j = (int)lane;
+        while (j >= nobj) { j -= nobj; ++ic; }
         const int npairs = nc * nobj;
-        int nw = 0;
         for (int qb = 0; qb < npairs; qb += 64) {
-            const int q = qb + (int)lane;
-            int ii = (int)((float)q * inv_nobj);
-            int j = q - ii * nobj;
-            ii = j < 0 ? ii - 1 : (j >= nobj ? ii + 1 : ii);
-            j = q - ii * nobj;
-            const int ic = min(ii, nc - 1);
-            const int i = a0 + ic;
-            const bool valid = q < npairs && j != nf + i;
-            const float hx = L.hx[i], hy = L.hy[i];
-            const float vx = L.ox[j] - L.ox[nf + i], vy = L.oy[j] - L.oy[nf + i];
-            const float f = vx * hx + vy * hy;   // along the heading
-            const float l = vx * hy - vy * hx;   // along r = (hy, -hx)
-            const uint32_t order = j < nf ? kOrderFood + (uint32_t)j : kOrderAgent + (uint32_t)(j - nf);
-            const float r2 = f * f + l * l;
-            const float A = f * f - 1.0f, B2 = 2.0f * (l * f), C = l * l - 1.0f;
-            const bool inwedge = valid && fabsf(l) <= fabsf(f) + kWedge;
-            // approximate roots bound the candidate pixels of the camera it faces
-            const bool fwd = f > 0.0f;
-            const float sq = __builtin_amdgcn_sqrtf(fmaxf(r2 - 1.0f, 0.0f));
-            const float ia = __builtin_amdgcn_rcpf(A);
-            const float u1 = (l * f - sq) * ia - kUEps, u2 = (l * f + sq) * ia + kUEps;
-            const float sc = fwd ? 12.0f : 4.0f, kmax = fwd ? 23.0f : 7.0f;
-            const float lo = fmaxf((u1 + 1.0f) * sc - 0.5f, -1.0f);
-            const float hi = fminf((u2 + 1.0f) * sc - 0.5f, kmax + 1.0f);
-            const int k0 = max((int)ceilf(lo), 0), k1 = min((int)floorf(hi), (int)kmax);
-            const int c = k1 - k0 + 1;
-            const bool wide = inwedge && (r2 <= 1.0f || fabsf(f) <= 1.5f || c > 3);
-            const bool narrow = inwedge && !wide;
-            const float z = zq(max0(fwd ? f - 1.0f : -f - 1.0f));
-            const uint32_t key = zkey(z, order);
-            uint32_t *kr = L.key + ic * kRays;
-            const int kb = fwd ? 0 : 24;
-#pragma unroll
-            for (int e = 0; e < 3; ++e) {
-                const int k = kb + min(k0 + e, (int)kmax);
-                const float u = L.u[k];
-                const float qv = (A * u - B2) * u + C;
-                const float p = f + u * l;
-                const bool hit = narrow && e < c && qv <= 0.0f && (fwd ? p > 0.0f : p < 0.0f);
-                if (hit) atomicMin(&kr[k], key);
+            bool keep = false;
+            float f = 0.0f, l = 0.0f;
+            if (ic < nc && j != nf + a0 + ic) {
+                uint32_t order;
+                pair_fl(L, nf, a0 + ic, j, f, l, order);
+                keep = fabsf(l) <= fabsf(f) + kWedge;
             }
-            if (narrow && fwd && C <= 0.0f) atomicMin(&kr[kSensor], key);   // finder ray
-            const uint64_t wm = ballot64(wide);
-            if (wide) L.wide[nw + (int)rank_below(wm)] = (uint32_t)ic | ((uint32_t)j << 8);
-            nw += __popcll(wm);
-            if (nw > kWideCap - 64) {
+            const uint64_t m = ballot64(keep);
+            if (keep) {
+                const int s = nq + (int)rank_below(m);
+                L.qcode[s] = (uint32_t)ic | ((uint32_t)j << 11);
+                L.qf[s] = f;
+                L.ql[s] = l;
+            }
+            nq += __popcll(m);
+            if (nq >= 64) {
                 wave_sync();
-                for (int e = 0; e < nw; ++e) wide_pair(L, a0, nf, L.wide[e]);
-                nw = 0;
+                run_survivors(L, nf, nq - 64, 64);
+                nq -= 64;
+            }
+            // advance the flattened (agent, object) index by 64
+            j += 64;
+            if (nobj >= 64) {
+                if (j >= nobj) { j -= nobj; ++ic; }
+            } else {
+                while (j >= nobj) { j -= nobj; ++ic; }
             }
         }
-        wave_sync();
-        for (int e = 0; e < nw; ++e) wide_pair(L, a0, nf, L.wide[e]);
+        if (nq > 0) {
+            wave_sync();
+            run_survivors(L, nf, 0, nq);
+        }
         wave_sync();
         // ---- output: keys vs walls, two agents per wave ----
         for (int pb = 0; pb < ((MB_ABL & 8) ? 0 : nc); pb += 2) {
@@ -857,18 +938,19 @@ __global__ __launch_bounds__(256) void sensor_kernel(SimState S, ObsTable nxt)
             const int px = (int)(lane & 31u);
             const bool valid = ci < nc;
             const int i = a0 + min(ci, nc - 1);
-            const float ox = L.ox[nf + i], oy = L.oy[nf + i], hx = L.hx[i], hy = L.hy[i];
+            const float2 p = L.obj[nf + i], h = L.hd[i];
+            const float4 a = make_float4(p.x, p.y, h.x, h.y);
             const float u = L.u[px];
             const float sgn = px < 24 ? 1.0f : -1.0f;
-            const float dx = sgn * (hx + u * hy), dy = sgn * (hy + u * (-hx));
+            const float dx = sgn * (a.z + u * a.w), dy = sgn * (a.w + u * (-a.z));
             const uint32_t kv = L.key[min(ci, nc - 1) * kRays + px];
             const float oz = __uint_as_float(kv & ~0xFFu);
             const uint32_t order = kv & 0xFFu;
-            const bool obj = kv != kNoKey && beats_wall(ox, oy, dx, dy, oz);
-            const int spv = L.sp[min((int)(order - kOrderAgent), n - 1) & 127];
+            const bool obj = kv != kNoKey && beats_wall(a.x, a.y, dx, dy, oz);
+            const int spv = (int)L.sp[min((int)(order - kOrderAgent), n - 1) & 127];
             const int sem = obj ? (order < kOrderAgent ? 6 : spv) : 5;
             float z = oz;
-            if (!obj) z = depth ? wall_z(ox, oy, dx, dy) : 0.0f;
+            if (!obj) z = depth ? wall_z(a.x, a.y, dx, dy) : 0.0f;
             uint32_t semv = (uint32_t)(uint8_t)(int8_t)sem << (8u * (lane & 3u));
             uint32_t depv = (uint32_t)depth_u8(z) << (8u * (lane & 3u));
             semv |= __shfl_xor(semv, 1);
@@ -885,11 +967,12 @@ __global__ __launch_bounds__(256) void sensor_kernel(SimState S, ObsTable nxt)
         }
         if ((int)lane < nc) {
             const int i = a0 + (int)lane;
+            const float2 p = L.obj[nf + i], h = L.hd[i];
+            const float4 a = make_float4(p.x, p.y, h.x, h.y);
             const uint32_t kv = L.key[lane * kRays + kSensor];
             const uint32_t order = kv & 0xFFu;
             const bool agent = kv != kNoKey && order >= kOrderAgent &&
-                               beats_wall(L.ox[nf + i], L.oy[nf + i], L.hx[i], L.hy[i],
-                                          __uint_as_float(kv & ~0xFFu));
+                               beats_wall(a.x, a.y, a.z, a.w, __uint_as_float(kv & ~0xFFu));
             S.finder[base + i] = agent ? (int32_t)(order - kOrderAgent) : -1;
         }
         wave_sync();
