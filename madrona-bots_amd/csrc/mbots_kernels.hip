@@ -631,12 +631,22 @@ __global__ __launch_bounds__(256) void move_kernel(const uint32_t *totals, const
 // oracle/mbots_oracle.c; culling only skips rays it proves cannot pass.
 // ---------------------------------------------------------------------------
 #ifndef MB_KEY_AGENTS
-#define MB_KEY_AGENTS 16
+#define MB_KEY_AGENTS 8
 #endif
 #ifndef MB_ABL
 #define MB_ABL 0                              // timing ablations: 1 no sensor work, 8 no output
 #endif
+#ifdef MB_PROF
+// per-phase shader-clock accounting (instrumentation builds only)
+__device__ unsigned long long g_sprof[8];
+#define PROF_NOW() __builtin_amdgcn_s_memtime()
+#define PROF_ADD(k, v) (prof[k] += (v))
+#else
+#define PROF_NOW() 0ull
+#define PROF_ADD(k, v) ((void)0)
+#endif
 constexpr int kKeyAgents = MB_KEY_AGENTS;     // agents per chunk (key rows)
+constexpr int kKeyStride = 36;                // key row: 32 pixels, finder, pad (16-B rows)
 constexpr int kQueueCap = 128;                // P1 survivors (flushed at >= 64)
 constexpr int kWideCap = 64;                  // wide pairs of one survivor batch
 constexpr int kMaxFood = kFoodCap + 2;        // live packages == currentNumFood <= 30
@@ -650,13 +660,11 @@ struct SensorLDS {
     float2 obj[kMaxFood + kMaxCap];           // positions: food, then agents
     float2 hd[kMaxCap];                       // agent headings
     int8_t sp[kMaxCap];
-    int32_t row[kMaxCap];                     // new export row per slot
-    uint32_t key[kKeyAgents * kRays];
-    uint32_t qcode[kQueueCap];                // P1 survivors: code, f, l
-    float qf[kQueueCap], ql[kQueueCap];
+    alignas(16) uint32_t key[kKeyAgents * kKeyStride];
+    uint32_t qcode[kQueueCap];                // P1 survivors: agent | object << 11
     uint32_t wcode[kWideCap];                 // wide pairs: code, f, l
     float wf[kWideCap], wl[kWideCap];
-    float u[kSensor];
+    alignas(16) float u[kSensor];
 };
 
 constexpr float kInLo = 0.0f + 0.2f;          // inner arena rectangle (walls, sim.cpp:157-194)
@@ -765,7 +773,7 @@ __device__ __forceinline__ void run_wide(SensorLDS &L, int nf, int cnt)
             const float f = L.wf[e], l = L.wl[e];
             const int ic = (int)(code & 0x1Fu), j = (int)(code >> 11);
             const uint32_t order = order_of(nf, j);
-            uint32_t *kr = L.key + ic * kRays;
+            uint32_t *kr = L.key + ic * kKeyStride;
             const int k = lane & 31;
             const uint32_t kv = pixel_key(f, l, L.u[k], k < 24, order);
             if (kv != kNoKey) atomicMin(&kr[k], kv);
@@ -777,7 +785,7 @@ __device__ __forceinline__ void run_wide(SensorLDS &L, int nf, int cnt)
 
 // P2: survivors [q0, q0 + cnt): approximate roots bound the candidate pixels;
 // <= 2 pixels + the finder are tested inline, wider pairs go to the wide list
-__device__ __forceinline__ void run_survivors(SensorLDS &L, int nf, int q0, int cnt)
+__device__ __forceinline__ void run_survivors(SensorLDS &L, int nf, int a0, int q0, int cnt)
 {
     if (MB_ABL & 16) return;
     const int lane = (int)__lane_id();
@@ -786,10 +794,9 @@ __device__ __forceinline__ void run_survivors(SensorLDS &L, int nf, int q0, int 
     float f = 0.0f, l = 0.0f;
     if (lane < cnt) {
         code = L.qcode[q0 + lane];
-        f = L.qf[q0 + lane];
-        l = L.ql[q0 + lane];
         const int ic = (int)(code & 0x1Fu), j = (int)(code >> 11);
-        const uint32_t order = order_of(nf, j);
+        uint32_t order;
+        pair_fl(L, nf, a0 + ic, j, f, l, order);
         const float r2 = f * f + l * l;
         if (r2 <= 1.0f || fabsf(f) <= 1.5f) {
             wide = true;
@@ -808,7 +815,7 @@ __device__ __forceinline__ void run_survivors(SensorLDS &L, int nf, int q0, int 
             if (c > 2) {
                 wide = true;
             } else if (!(MB_ABL & 32)) {
-                uint32_t *kr = L.key + ic * kRays;
+                uint32_t *kr = L.key + ic * kKeyStride;
                 const float ua = L.u[k0 & 31], ub = L.u[(k0 + 1) & 31];
                 const uint32_t ka = pixel_key(f, l, ua, fwd, order);
                 const uint32_t kb = pixel_key(f, l, ub, fwd, order);
@@ -834,6 +841,31 @@ __device__ __forceinline__ void run_survivors(SensorLDS &L, int nf, int q0, int 
     }
 }
 
+// the world's staged inputs, loaded as one batch of independent loads
+struct SensorPrefetch {
+    uint64_t food;             // lane < 48: packed chunk record
+    float x, y, rw, rz;        // lane < min(cap, 64): agent slot `lane`
+    int32_t sp, row;
+    int n;
+};
+
+__device__ __forceinline__ void sensor_prefetch(const SimState &S, uint32_t w, uint32_t lane,
+                                                SensorPrefetch &p)
+{
+    p.n = S.n[w];
+    p.food = lane < kNumChunks ? S.food[(size_t)w * kNumChunks + lane] : 0ull;
+    if (lane < S.cap) {   // rows past n are allocated (stale); only [0, n) is staged
+        const size_t i = (size_t)w * S.cap + lane;
+        p.x = S.x[i];
+        p.y = S.y[i];
+        p.rw = S.rw[i];
+        p.rz = S.rz[i];
+        p.sp = S.species[i];
+        p.row = S.obsrow[i];
+    }
+}
+
+// one wave per world, 4 worlds per block
 __global__ __launch_bounds__(256) void sensor_kernel(SimState S, ObsTable nxt)
 {
     __shared__ SensorLDS lds[kWorldsPerBlock];
@@ -842,16 +874,23 @@ __global__ __launch_bounds__(256) void sensor_kernel(SimState S, ObsTable nxt)
     const uint32_t w = blockIdx.x * kWorldsPerBlock + wv;
     if (w >= S.W) return;
     SensorLDS &L = lds[wv];
-    const size_t base = (size_t)w * S.cap;
-    const int n = S.n[w];
     const bool depth = (S.flags & kFlagFixDepth) != 0;
+#ifdef MB_PROF
+    unsigned long long prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#endif
     if (lane < kSensor) L.u[lane] = kURay[lane];
+    SensorPrefetch pf;
+    sensor_prefetch(S, w, lane, pf);
+    do {
+    const unsigned long long t_start = PROF_NOW();
+    const size_t base = (size_t)w * S.cap;
+    const SensorPrefetch cur = pf;
+    const int n = cur.n;
 
     // ---- live food packages in (chunk, package) order -> objects [0, nf) ----
     int nf;
     {
-        uint64_t rec = 0;
-        if (lane < kNumChunks) rec = S.food[(size_t)w * kNumChunks + lane];
+        const uint64_t rec = cur.food;
         const uint32_t live = (uint32_t)(rec >> 40) & 31u;
         const int cnt = __popc(live);
         int off = 0, tot = 0;
@@ -876,22 +915,33 @@ __global__ __launch_bounds__(256) void sensor_kernel(SimState S, ObsTable nxt)
         nf = min(tot, kMaxFood);
     }
     // ---- agents -> objects [nf, nf + n) ----
-    for (int i = lane; i < n; i += 64) {
+    if ((int)lane < n) {
+        float hx, hy;
+        heading(cur.rw, cur.rz, hx, hy);
+        L.obj[nf + lane] = make_float2(cur.x, cur.y);
+        L.hd[lane] = make_float2(hx, hy);
+        L.sp[lane] = (int8_t)cur.sp;
+    }
+    // export rows stay in registers: lane s holds slot s (row_lo) and 64 + s (row_hi)
+    const int row_lo = cur.row;
+    int row_hi = 0;
+    if (64 + (int)lane < n) {   // slots past 64: loaded here
+        const int i = 64 + (int)lane;
         float hx, hy;
         heading(S.rw[base + i], S.rz[base + i], hx, hy);
-        const float x = S.x[base + i], y = S.y[base + i];
-        L.obj[nf + i] = make_float2(x, y);
+        L.obj[nf + i] = make_float2(S.x[base + i], S.y[base + i]);
         L.hd[i] = make_float2(hx, hy);
         L.sp[i] = (int8_t)S.species[base + i];
-        L.row[i] = S.obsrow[base + i];
+        row_hi = S.obsrow[base + i];
     }
-    if (MB_ABL & 1) return;
+    if (MB_ABL & 1) continue;
     const int nobj = nf + n;
     wave_sync();
+    PROF_ADD(0, PROF_NOW() - t_start);
 
     for (int a0 = 0; a0 < n; a0 += kKeyAgents) {
         const int nc = min(kKeyAgents, n - a0);
-        for (int q = lane; q < nc * kRays; q += 64) L.key[q] = kNoKey;
+        for (int q = lane; q < nc * kKeyStride; q += 64) L.key[q] = kNoKey;
         wave_sync();
         // ---- P1: wedge pre-cull of the chunk's (agent, object) pairs ----
         int nq = 0;
@@ -900,23 +950,21 @@ __global__ __launch_bounds__(256) void sensor_kernel(SimState S, ObsTable nxt)
         const int npairs = nc * nobj;
         for (int qb = 0; qb < npairs; qb += 64) {
             bool keep = false;
-            float f = 0.0f, l = 0.0f;
             if (ic < nc && j != nf + a0 + ic) {
+                float f, l;
                 uint32_t order;
                 pair_fl(L, nf, a0 + ic, j, f, l, order);
                 keep = fabsf(l) <= fabsf(f) + kWedge;
             }
             const uint64_t m = ballot64(keep);
-            if (keep) {
-                const int s = nq + (int)rank_below(m);
-                L.qcode[s] = (uint32_t)ic | ((uint32_t)j << 11);
-                L.qf[s] = f;
-                L.ql[s] = l;
-            }
+            if (keep) L.qcode[nq + (int)rank_below(m)] = (uint32_t)ic | ((uint32_t)j << 11);
             nq += __popcll(m);
             if (nq >= 64) {
                 wave_sync();
-                run_survivors(L, nf, nq - 64, 64);
+                const unsigned long long ta = PROF_NOW();
+                run_survivors(L, nf, a0, nq - 64, 64);
+                PROF_ADD(2, PROF_NOW() - ta);
+                PROF_ADD(5, 64);
                 nq -= 64;
             }
             // advance the flattened (agent, object) index by 64
@@ -929,55 +977,84 @@ __global__ __launch_bounds__(256) void sensor_kernel(SimState S, ObsTable nxt)
         }
         if (nq > 0) {
             wave_sync();
-            run_survivors(L, nf, 0, nq);
+            const unsigned long long ta = PROF_NOW();
+            run_survivors(L, nf, a0, 0, nq);
+            PROF_ADD(2, PROF_NOW() - ta);
+            PROF_ADD(5, nq);
         }
         wave_sync();
-        // ---- output: keys vs walls, two agents per wave ----
-        for (int pb = 0; pb < ((MB_ABL & 8) ? 0 : nc); pb += 2) {
-            const int ci = pb + (int)(lane >> 5);
-            const int px = (int)(lane & 31u);
-            const bool valid = ci < nc;
-            const int i = a0 + min(ci, nc - 1);
+        const unsigned long long to = PROF_NOW();
+        // ---- output: keys vs walls; lane = (agent ci, pixels 4g .. 4g+3) ----
+        if (!(MB_ABL & 8)) {
+            const int ci = (int)(lane >> 3), g = (int)(lane & 7u);
+            const int cc = min(ci, nc - 1);
+            const int i = a0 + cc;
             const float2 p = L.obj[nf + i], h = L.hd[i];
-            const float4 a = make_float4(p.x, p.y, h.x, h.y);
-            const float u = L.u[px];
-            const float sgn = px < 24 ? 1.0f : -1.0f;
-            const float dx = sgn * (a.z + u * a.w), dy = sgn * (a.w + u * (-a.z));
-            const uint32_t kv = L.key[min(ci, nc - 1) * kRays + px];
-            const float oz = __uint_as_float(kv & ~0xFFu);
-            const uint32_t order = kv & 0xFFu;
-            const bool obj = kv != kNoKey && beats_wall(a.x, a.y, dx, dy, oz);
-            const int spv = (int)L.sp[min((int)(order - kOrderAgent), n - 1) & 127];
-            const int sem = obj ? (order < kOrderAgent ? 6 : spv) : 5;
-            float z = oz;
-            if (!obj) z = depth ? wall_z(a.x, a.y, dx, dy) : 0.0f;
-            uint32_t semv = (uint32_t)(uint8_t)(int8_t)sem << (8u * (lane & 3u));
-            uint32_t depv = (uint32_t)depth_u8(z) << (8u * (lane & 3u));
-            semv |= __shfl_xor(semv, 1);
-            semv |= __shfl_xor(semv, 2);
-            if (depth) {
-                depv |= __shfl_xor(depv, 1);
-                depv |= __shfl_xor(depv, 2);
+            const uint4 kv4 = *reinterpret_cast<const uint4 *>(&L.key[cc * kKeyStride + 4 * g]);
+            const float4 u4 = *reinterpret_cast<const float4 *>(&L.u[4 * g]);
+            const int r = a0 < 64 ? __shfl(row_lo, i & 63) : __shfl(row_hi, i & 63);
+            const float sgn = g < 6 ? 1.0f : -1.0f;
+            const uint32_t kvs[4] = {kv4.x, kv4.y, kv4.z, kv4.w};
+            const float us[4] = {u4.x, u4.y, u4.z, u4.w};
+            uint32_t semv = 0, depv = 0;
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const float u = us[t];
+                const float dx = sgn * (h.x + u * h.y), dy = sgn * (h.y + u * (-h.x));
+                const uint32_t kv = kvs[t];
+                const float oz = __uint_as_float(kv & ~0xFFu);
+                const uint32_t order = kv & 0xFFu;
+                const bool obj = (kv != kNoKey) & beats_wall(p.x, p.y, dx, dy, oz);
+                const int spv = (int)L.sp[min((int)(order - kOrderAgent), n - 1) & 127];
+                const int sem = obj ? (order < kOrderAgent ? 6 : spv) : 5;
+                semv |= (uint32_t)(uint8_t)(int8_t)sem << (8 * t);
+                if (depth) {
+                    const float z = obj ? oz : wall_z(p.x, p.y, dx, dy);
+                    depv |= (uint32_t)depth_u8(z) << (8 * t);
+                }
             }
-            if (valid && (lane & 3u) == 0u) {
-                const size_t r = (size_t)L.row[i];
-                reinterpret_cast<uint32_t *>(nxt.sem + r * kSensor)[px >> 2] = semv;
-                if (depth) reinterpret_cast<uint32_t *>(nxt.depth + r * kSensor)[px >> 2] = depv;
+            if (ci < nc) {
+                reinterpret_cast<uint32_t *>(nxt.sem + (size_t)r * kSensor)[g] = semv;
+                if (depth) reinterpret_cast<uint32_t *>(nxt.depth + (size_t)r * kSensor)[g] = depv;
             }
         }
         if ((int)lane < nc) {
             const int i = a0 + (int)lane;
             const float2 p = L.obj[nf + i], h = L.hd[i];
             const float4 a = make_float4(p.x, p.y, h.x, h.y);
-            const uint32_t kv = L.key[lane * kRays + kSensor];
+            const uint32_t kv = L.key[lane * kKeyStride + kSensor];
             const uint32_t order = kv & 0xFFu;
             const bool agent = kv != kNoKey && order >= kOrderAgent &&
                                beats_wall(a.x, a.y, a.z, a.w, __uint_as_float(kv & ~0xFFu));
             S.finder[base + i] = agent ? (int32_t)(order - kOrderAgent) : -1;
         }
         wave_sync();
+        PROF_ADD(3, PROF_NOW() - to);
     }
+#ifdef MB_PROF
+    prof[4] += PROF_NOW() - t_start;
+    prof[6] += (unsigned long long)n * (unsigned long long)(nf + n);
+    prof[7] += 1;
+#endif
+    } while (false);
+#ifdef MB_PROF
+    if (lane < 8) {
+        unsigned long long v = 0;
+        for (int k = 0; k < 8; ++k) v = (int)lane == k ? prof[k] : v;
+        atomicAdd(&g_sprof[lane], v);
+    }
+#endif
 }
+
+#ifdef MB_PROF
+extern "C" __attribute__((visibility("default"))) int mbots_debug_sensor_prof(unsigned long long *out)
+{
+    static const unsigned long long zero[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sprof), sizeof(zero)) != hipSuccess) return -1;
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_sprof), zero, sizeof(zero)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 // ---------------------------------------------------------------------------
 // K5: shiftObservationsSystem + shiftHiddenState (sim.cpp:1002-1048): Prev* <-
