@@ -14,6 +14,18 @@
 
 namespace mbots {
 
+#ifdef MB_PROF
+// per-phase shader-clock accounting (instrumentation builds only)
+// 64 slots per counter (by block) keep the accounting atomics uncontended
+__device__ unsigned long long g_sprof[64 * 8];
+__device__ unsigned long long g_kprof[64 * 8];
+#define PROF_NOW() __builtin_amdgcn_s_memtime()
+#define PROF_ADD(k, v) (prof[k] += (v))
+#else
+#define PROF_NOW() 0ull
+#define PROF_ADD(k, v) ((void)0)
+#endif
+
 constexpr int kWorldsPerBlock = 4;
 constexpr int kTileWorlds = 1024;             // worlds per scan tile (K2 block)
 
@@ -48,12 +60,16 @@ __device__ __forceinline__ uint64_t food_pack(const uint32_t *pk)
 // ---------------------------------------------------------------------------
 struct WorldLDS {
     float x[kMaxCap], y[kMaxCap], rw[kMaxCap], rz[kMaxCap];
-    int32_t species[kMaxCap], accum[kMaxCap], finder[kMaxCap], obsrow[kMaxCap];
-    int32_t key[kMaxCap], take[kMaxCap];
-    uint32_t flags[kMaxCap];
-    float sur0[kMaxCap], sur1[kMaxCap];
+    int32_t accum[kMaxCap], obsrow[kMaxCap];
+    int8_t species[kMaxCap], finder[kMaxCap];
+    uint8_t flags[kMaxCap];
+    // healthSync's cell keys / package takes (slots < n0) share storage with the
+    // surroundings written after it; children/respawns (slots >= n0) only
+    // touch the sur half
+    union { int32_t key[kMaxCap]; float sur0[kMaxCap]; };
+    union { int32_t take[kMaxCap]; float sur1[kMaxCap]; };
     uint32_t food[kNumPkg];
-    uint32_t nag[kNumChunks], spd[kNumChunks];
+    uint32_t chunk[kNumChunks];   // ChunkInfo: numAgents << 16 | totalSpeed (<= 128 x 2)
     uint32_t cnt[kNumSpecies], hsum[kNumSpecies];
     int32_t need[kNumSpecies];
     int32_t scount[kNumSpecies];
@@ -82,11 +98,11 @@ __device__ __forceinline__ void init_slot(WorldLDS &L, int s, float x, float y, 
     L.y[s] = y;
     L.rw[s] = 1.0f;
     L.rz[s] = 0.0f;
-    L.species[s] = sp;
+    L.species[s] = (int8_t)sp;
     L.accum[s] = h;
     L.finder[s] = -1;
     L.obsrow[s] = -1;
-    L.flags[s] = F_ALIVE;
+    L.flags[s] = (uint8_t)F_ALIVE;
     L.sur0[s] = 0.0f;
     L.sur1[s] = 0.0f;
 }
@@ -128,66 +144,88 @@ __device__ void world_step(SimState &S, const ObsTable &cur, WorldLDS &L, uint32
     const uint32_t cap = S.cap;
     const size_t base = (size_t)w * cap;
     const int n0 = S.n[w];
+#ifdef MB_PROF
+    unsigned long long prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long tp = PROF_NOW(), tq;
+#define KPROF(k) (tq = PROF_NOW(), prof[k] += tq - tp, tp = tq)
+#else
+#define KPROF(k) ((void)0)
+#endif
 
-    // ---- stage the world in LDS ----
+    // ---- stage the world in LDS; slot `lane`'s action row is fetched now and
+    // consumed after addFood (its latency hides behind that serial phase) ----
+    int2 pa0 = make_int2(0, 0), pa1 = pa0, pa2 = pa0;
     for (int i = lane; i < n0; i += 64) {
+        const int32_t row = S.obsrow[base + i];
+        if (i < 64 && row >= 0) {
+            const int2 *ap = reinterpret_cast<const int2 *>(cur.action + (size_t)row * 6);
+            pa0 = ap[0]; pa1 = ap[1]; pa2 = ap[2];
+        }
         L.x[i] = S.x[base + i];
         L.y[i] = S.y[base + i];
         L.rw[i] = S.rw[base + i];
         L.rz[i] = S.rz[base + i];
-        L.species[i] = S.species[base + i];
+        L.species[i] = (int8_t)S.species[base + i];
         L.accum[i] = S.health[base + i];
-        L.finder[i] = S.finder[base + i];
-        L.obsrow[i] = S.obsrow[base + i];
-        L.flags[i] = F_ALIVE;
+        L.finder[i] = (int8_t)S.finder[base + i];
+        L.obsrow[i] = row;
+        L.flags[i] = (uint8_t)F_ALIVE;
     }
     if (lane < kNumChunks) food_unpack(S.food[(size_t)w * kNumChunks + lane], &L.food[lane * kMaxPkg]);
-    if (lane < kNumChunks) { L.nag[lane] = 0u; L.spd[lane] = 0u; }   // resetChunkInfoSystem
+    if (lane < kNumChunks) L.chunk[lane] = 0u;   // resetChunkInfoSystem
     if (lane < kNumSpecies) { L.cnt[lane] = 0u; L.hsum[lane] = 0u; L.scount[lane] = 0; }
     if (lane == 0) L.consumed = 0;
     const uint2 key = S.key[w];
     uint32_t ctr = S.ctr[w];
     int32_t cur_food = S.cur_food[w];
     wave_sync();
+    KPROF(0);
 
-    // ---- addFoodSystem (sim.cpp:363-387) + addFoodToChunk (:308-361), serial ----
-    if (lane == 0) {
-        if (sample_i32(rng_draw(key, ctr++), 0, 10) == 0) {
-            uint32_t nf = (uint32_t)sample_i32(rng_draw(key, ctr++), 1, 3);
-            uint32_t diff = (uint32_t)kFoodCap - (uint32_t)cur_food;
-            if (diff < nf) nf = diff;
-            for (uint32_t f = 0; f < nf; ++f) {
-                uint32_t cx = (uint32_t)sample_i32(rng_draw(key, ctr++), 0, kChunksX);
-                uint32_t cy = (uint32_t)sample_i32(rng_draw(key, ctr++), 0, kChunksY);
-                int chunk = (int)(cx + cy * kChunksX);
-                ctr += 2;   // two unused draws (sim.cpp:311-312)
-                for (int k = 0; k < kMaxPkg; ++k) {
-                    uint32_t p = L.food[chunk * kMaxPkg + k];
+    // ---- addFoodSystem (sim.cpp:363-387) + addFoodToChunk (:308-361) ----
+    // The serial draw sequence uses at most 2 + 3 x 7 = 23 counters: lane k
+    // computes draw ctr + k up front and the (wave-uniform) logic reads them
+    // with readlane.
+    {
+        const uint32_t dl = rng_draw(key, ctr + (lane & 31u));
+        auto D = [&](uint32_t k) { return (uint32_t)__builtin_amdgcn_readlane((int)dl, (int)k); };
+        uint32_t k = 0;
+        if (sample_i32(D(k++), 0, 10) == 0) {
+            uint32_t nfood = (uint32_t)sample_i32(D(k++), 1, 3);
+            const uint32_t diff = (uint32_t)kFoodCap - (uint32_t)cur_food;
+            if (diff < nfood) nfood = diff;
+            for (uint32_t f = 0; f < nfood; ++f) {
+                const uint32_t cx = (uint32_t)sample_i32(D(k++), 0, kChunksX);
+                const uint32_t cy = (uint32_t)sample_i32(D(k++), 0, kChunksY);
+                const int chunk = (int)(cx + cy * kChunksX);
+                k += 2;   // two unused draws (sim.cpp:311-312)
+                for (int q = 0; q < kMaxPkg; ++q) {
+                    const uint32_t p = L.food[chunk * kMaxPkg + q];
                     if ((p >> 16) == 0u) {
-                        uint32_t rx = (uint32_t)sample_i32(rng_draw(key, ctr++), 0, kChunkW);
-                        uint32_t ry = (uint32_t)sample_i32(rng_draw(key, ctr++), 0, kChunkW);
-                        L.food[chunk * kMaxPkg + k] = (rx & 0xFFu) | ((ry & 0xFFu) << 8) | (1u << 16);
-                        ctr += 1;   // food entity rotation draw (sim.cpp:338-341)
+                        const uint32_t rx = (uint32_t)sample_i32(D(k++), 0, kChunkW);
+                        const uint32_t ry = (uint32_t)sample_i32(D(k++), 0, kChunkW);
+                        if (lane == 0)
+                            L.food[chunk * kMaxPkg + q] = (rx & 0xFFu) | ((ry & 0xFFu) << 8) | (1u << 16);
+                        k += 1;   // food entity rotation draw (sim.cpp:338-341)
                         cur_food += 1;
                         break;
                     }
                 }
+                wave_sync();
             }
         }
+        ctr += k;
     }
-    ctr = __shfl(ctr, 0);
-    cur_food = __shfl(cur_food, 0);
-    wave_sync();
+    KPROF(1);
 
     // ---- actionSystem (sim.cpp:419-502) ----
     for (int i = lane; i < n0; i += 64) {
-        int32_t act[6] = {0, 0, 0, 0, 0, 0};
+        int2 a0 = pa0, a1 = pa1, a2 = pa2;
         const int32_t row = L.obsrow[i];
-        if (row >= 0) {
+        if (i >= 64 && row >= 0) {
             const int2 *ap = reinterpret_cast<const int2 *>(cur.action + (size_t)row * 6);
-            int2 a0 = ap[0], a1 = ap[1], a2 = ap[2];
-            act[0] = a0.x; act[1] = a0.y; act[2] = a1.x; act[3] = a1.y; act[4] = a2.x; act[5] = a2.y;
+            a0 = ap[0]; a1 = ap[1]; a2 = ap[2];
         }
+        const int32_t act[6] = {a0.x, a0.y, a1.x, a1.y, a2.x, a2.y};
         const int32_t sp = L.species[i];
         uint32_t fl = F_ALIVE | (act[5] ? F_BREED : 0u);
         const int32_t tgt = L.finder[i];
@@ -216,12 +254,12 @@ __device__ void world_step(SimState &S, const ObsTable &cur, WorldLDS &L, uint32
         float ddx = x - ox, ddy = y - oy;
         float len = sqrtf(ddx * ddx + ddy * ddy);
         int32_t ci = chunk_index(floorf((x / 1.0f) / 16.0f), floorf((y / 1.0f) / 16.0f));
-        atomicAdd(&L.nag[ci], 1u);
-        atomicAdd(&L.spd[ci], (uint32_t)(len * 2.0f));
+        atomicAdd(&L.chunk[ci], (1u << 16) + (uint32_t)(len * 2.0f));
         L.x[i] = x; L.y[i] = y; L.rw[i] = rw; L.rz[i] = rz;
-        L.flags[i] = fl;
+        L.flags[i] = (uint8_t)fl;
     }
     wave_sync();
+    KPROF(2);
 
     // ---- healthSync (sim.cpp:505-581) ----
     // food: the k-th agent (slot order) standing on a cell takes the k-th live
@@ -286,7 +324,7 @@ __device__ void world_step(SimState &S, const ObsTable &cur, WorldLDS &L, uint32
             }
             if (h <= 0) fl &= ~F_ALIVE;
             L.accum[i] = h;
-            L.flags[i] = fl;
+            L.flags[i] = (uint8_t)fl;
         }
         const uint64_t m = ballot64(want_child);
         if (want_child) {
@@ -299,6 +337,7 @@ __device__ void world_step(SimState &S, const ObsTable &cur, WorldLDS &L, uint32
         else n1 += made;
     }
     wave_sync();
+    KPROF(3);
     cur_food -= L.consumed;
 
     // ---- updateSurroundingObservation (sim.cpp:583-654) + tracker (:719-734) ----
@@ -312,14 +351,12 @@ __device__ void world_step(SimState &S, const ObsTable &cur, WorldLDS &L, uint32
         int32_t i00 = chunk_index(x0, y0), i10 = chunk_index(x1, y0);
         int32_t i01 = chunk_index(x0, y1), i11 = chunk_index(x1, y1);
         float xi = chx - x0, yi = chy - y0;
-        float n00 = i00 >= 0 ? (float)L.nag[i00] : 0.0f;
-        float n10 = i10 >= 0 ? (float)L.nag[i10] : 0.0f;
-        float n01 = i01 >= 0 ? (float)L.nag[i01] : 0.0f;
-        float n11 = i11 >= 0 ? (float)L.nag[i11] : 0.0f;
-        float s00 = i00 >= 0 ? (float)L.spd[i00] : 0.0f;
-        float s10 = i10 >= 0 ? (float)L.spd[i10] : 0.0f;
-        float s01 = i01 >= 0 ? (float)L.spd[i01] : 0.0f;
-        float s11 = i11 >= 0 ? (float)L.spd[i11] : 0.0f;
+        const uint32_t c00 = i00 >= 0 ? L.chunk[i00] : 0u, c10 = i10 >= 0 ? L.chunk[i10] : 0u;
+        const uint32_t c01 = i01 >= 0 ? L.chunk[i01] : 0u, c11 = i11 >= 0 ? L.chunk[i11] : 0u;
+        float n00 = (float)(c00 >> 16), n10 = (float)(c10 >> 16);
+        float n01 = (float)(c01 >> 16), n11 = (float)(c11 >> 16);
+        float s00 = (float)(c00 & 0xFFFFu), s10 = (float)(c10 & 0xFFFFu);
+        float s01 = (float)(c01 & 0xFFFFu), s11 = (float)(c11 & 0xFFFFu);
         float nx0 = xi * n10 + (1.0f - xi) * n00;
         float nx1 = xi * n11 + (1.0f - xi) * n01;
         float sx0 = xi * s10 + (1.0f - xi) * s00;
@@ -356,6 +393,7 @@ __device__ void world_step(SimState &S, const ObsTable &cur, WorldLDS &L, uint32
     int n2 = n1 + total_need;
     if (n2 > (int)cap) { ovf += (uint32_t)(n2 - (int)cap); n2 = (int)cap; }
     wave_sync();
+    KPROF(4);
 
     // ---- compaction (SortArchetypeNode<Agent, WorldID>, sim.cpp:1129) ----
     int nn = 0;
@@ -388,6 +426,16 @@ __device__ void world_step(SimState &S, const ObsTable &cur, WorldLDS &L, uint32
         S.cur_food[w] = cur_food;
         if (ovf) S.overflow[w] += ovf;
     }
+    KPROF(5);
+#ifdef MB_PROF
+    prof[6] = (unsigned long long)n0;
+    prof[7] = 1;
+    if (lane < 8) {
+        unsigned long long v = 0;
+        for (int k = 0; k < 8; ++k) v = (int)lane == k ? prof[k] : v;
+        atomicAdd(&g_kprof[(blockIdx.x & 63u) * 8 + lane], v);
+    }
+#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -635,15 +683,6 @@ __global__ __launch_bounds__(256) void move_kernel(const uint32_t *totals, const
 #endif
 #ifndef MB_ABL
 #define MB_ABL 0                              // timing ablations: 1 no sensor work, 8 no output
-#endif
-#ifdef MB_PROF
-// per-phase shader-clock accounting (instrumentation builds only)
-__device__ unsigned long long g_sprof[8];
-#define PROF_NOW() __builtin_amdgcn_s_memtime()
-#define PROF_ADD(k, v) (prof[k] += (v))
-#else
-#define PROF_NOW() 0ull
-#define PROF_ADD(k, v) ((void)0)
 #endif
 constexpr int kKeyAgents = MB_KEY_AGENTS;     // agents per chunk (key rows)
 constexpr int kKeyStride = 36;                // key row: 32 pixels, finder, pad (16-B rows)
@@ -1041,7 +1080,7 @@ __global__ __launch_bounds__(256) void sensor_kernel(SimState S, ObsTable nxt)
     if (lane < 8) {
         unsigned long long v = 0;
         for (int k = 0; k < 8; ++k) v = (int)lane == k ? prof[k] : v;
-        atomicAdd(&g_sprof[lane], v);
+        atomicAdd(&g_sprof[(blockIdx.x & 63u) * 8 + lane], v);
     }
 #endif
 }
@@ -1049,10 +1088,19 @@ __global__ __launch_bounds__(256) void sensor_kernel(SimState S, ObsTable nxt)
 #ifdef MB_PROF
 extern "C" __attribute__((visibility("default"))) int mbots_debug_sensor_prof(unsigned long long *out)
 {
-    static const unsigned long long zero[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    static unsigned long long buf[64 * 8], zero[64 * 8];
     if (hipDeviceSynchronize() != hipSuccess) return -1;
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sprof), sizeof(zero)) != hipSuccess) return -1;
-    return hipMemcpyToSymbol(HIP_SYMBOL(g_sprof), zero, sizeof(zero)) == hipSuccess ? 0 : -1;
+    for (int t = 0; t < 2; ++t) {
+        const void *sym = t == 0 ? HIP_SYMBOL(g_sprof) : HIP_SYMBOL(g_kprof);
+        if (hipMemcpyFromSymbol(buf, sym, sizeof(buf)) != hipSuccess) return -1;
+        if (hipMemcpyToSymbol(sym, zero, sizeof(zero)) != hipSuccess) return -1;
+        for (int k = 0; k < 8; ++k) {
+            unsigned long long v = 0;
+            for (int b = 0; b < 64; ++b) v += buf[b * 8 + k];
+            out[t * 8 + k] = v;
+        }
+    }
+    return 0;
 }
 #endif
 
