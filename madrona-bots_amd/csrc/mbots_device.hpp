@@ -100,6 +100,12 @@ __device__ __forceinline__ uint8_t depth_u8(float t)
 // ---------------------------------------------------------------------------
 // Wave-level helpers (wave64)
 // ---------------------------------------------------------------------------
+// a wave-uniform value in an SGPR: the compiler cannot prove that the world
+// index (threadIdx.x >> 6) or a value loaded at it is uniform, and would keep
+// loop bounds in VGPRs (exec-masked loops, per-lane loads)
+__device__ __forceinline__ uint32_t uniform(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+__device__ __forceinline__ int32_t uniform(int32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+
 __device__ __forceinline__ void wave_sync()
 {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");

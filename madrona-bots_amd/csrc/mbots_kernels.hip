@@ -11,6 +11,7 @@
 // counts) -> K2 scan (species-major row offsets) -> K3 export_sensor (row move,
 // observations, reward, raycast sensor) ; shift_observations = K5 shift.
 #include "mbots_kernels.hpp"
+#include "mbots_ray.hpp"
 
 namespace mbots {
 
@@ -32,25 +33,26 @@ constexpr int kTileWorlds = 1024;             // worlds per scan tile (K2 block)
 // ---------------------------------------------------------------------------
 // Food packages: HBM keeps one 8-byte record per chunk (5 x (x | y << 4) bytes,
 // live mask in byte 5: kMaxFoodPerPackage = 1, so numFood is a bit);
-// LDS keeps one u32 per package: x | y << 8 | numFood << 16.
+// LDS keeps one u16 per package: x | y << 4 | numFood << 8.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ void food_unpack(uint64_t rec, uint32_t *pk)
+constexpr uint32_t kPkgLive = 1u << 8;
+__device__ __forceinline__ void food_unpack(uint64_t rec, uint16_t *pk)
 {
 #pragma unroll
     for (int k = 0; k < kMaxPkg; ++k) {
         const uint32_t xy = (uint32_t)(rec >> (8 * k)) & 0xFFu;
         const uint32_t live = (uint32_t)(rec >> (40 + k)) & 1u;
-        pk[k] = (xy & 15u) | ((xy >> 4) << 8) | (live << 16);
+        pk[k] = (uint16_t)(xy | (live << 8));
     }
 }
-__device__ __forceinline__ uint64_t food_pack(const uint32_t *pk)
+__device__ __forceinline__ uint64_t food_pack(const uint16_t *pk)
 {
     uint64_t rec = 0;
 #pragma unroll
     for (int k = 0; k < kMaxPkg; ++k) {
         const uint32_t p = pk[k];
-        rec |= (uint64_t)((p & 15u) | (((p >> 8) & 15u) << 4)) << (8 * k);
-        rec |= (uint64_t)((p >> 16) & 1u) << (40 + k);
+        rec |= (uint64_t)(p & 0xFFu) << (8 * k);
+        rec |= (uint64_t)((p >> 8) & 1u) << (40 + k);
     }
     return rec;
 }
@@ -64,11 +66,13 @@ struct WorldLDS {
     int8_t species[kMaxCap], finder[kMaxCap];
     uint8_t flags[kMaxCap];
     // healthSync's cell keys / package takes (slots < n0) share storage with the
-    // surroundings written after it; children/respawns (slots >= n0) only
-    // touch the sur half
-    union { int32_t key[kMaxCap]; float sur0[kMaxCap]; };
-    union { int32_t take[kMaxCap]; float sur1[kMaxCap]; };
-    uint32_t food[kNumPkg];
+    // surroundings written after it (children/respawns, slots >= n0, only
+    // touch the sur half)
+    union {
+        struct { int32_t key[kMaxCap]; int32_t take[kMaxCap]; };
+        struct { float sur0[kMaxCap]; float sur1[kMaxCap]; };
+    };
+    uint16_t food[kNumPkg];
     uint32_t chunk[kNumChunks];   // ChunkInfo: numAgents << 16 | totalSpeed (<= 128 x 2)
     uint32_t cnt[kNumSpecies], hsum[kNumSpecies];
     int32_t need[kNumSpecies];
@@ -122,7 +126,7 @@ __global__ __launch_bounds__(256) void world_step_kernel(SimState S, ObsTable cu
     __shared__ int32_t blk[kWorldsPerBlock][5];
     const uint32_t wv = threadIdx.x >> 6;
     const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t w = blockIdx.x * kWorldsPerBlock + wv;
+    const uint32_t w = uniform(blockIdx.x * kWorldsPerBlock + wv);
     if (w < S.W) world_step(S, cur, lds[wv], w, lane);
     // per-block species/agent counts -> the K2 scan tile (one atomic per counter)
     if (lane < 5) {
@@ -143,7 +147,7 @@ __device__ void world_step(SimState &S, const ObsTable &cur, WorldLDS &L, uint32
 {
     const uint32_t cap = S.cap;
     const size_t base = (size_t)w * cap;
-    const int n0 = S.n[w];
+    const int n0 = uniform(S.n[w]);
 #ifdef MB_PROF
     unsigned long long prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     unsigned long long tp = PROF_NOW(), tq;
@@ -200,11 +204,11 @@ __device__ void world_step(SimState &S, const ObsTable &cur, WorldLDS &L, uint32
                 k += 2;   // two unused draws (sim.cpp:311-312)
                 for (int q = 0; q < kMaxPkg; ++q) {
                     const uint32_t p = L.food[chunk * kMaxPkg + q];
-                    if ((p >> 16) == 0u) {
+                    if ((p & kPkgLive) == 0u) {
                         const uint32_t rx = (uint32_t)sample_i32(D(k++), 0, kChunkW);
                         const uint32_t ry = (uint32_t)sample_i32(D(k++), 0, kChunkW);
                         if (lane == 0)
-                            L.food[chunk * kMaxPkg + q] = (rx & 0xFFu) | ((ry & 0xFFu) << 8) | (1u << 16);
+                            L.food[chunk * kMaxPkg + q] = (uint16_t)((rx & 15u) | ((ry & 15u) << 4) | kPkgLive);
                         k += 1;   // food entity rotation draw (sim.cpp:338-341)
                         cur_food += 1;
                         break;
@@ -276,19 +280,16 @@ __device__ void world_step(SimState &S, const ObsTable &cur, WorldLDS &L, uint32
         const int32_t kk = L.key[i];
         const int ci = kk >> 8;
         const uint32_t cx = (uint32_t)kk & 15u, cy = ((uint32_t)kk >> 4) & 15u;
+        const uint32_t cell = cx | (cy << 4) | kPkgLive;   // a live package on this cell
         int navail = 0;
-        for (int k = 0; k < kMaxPkg; ++k) {
-            uint32_t p = L.food[ci * kMaxPkg + k];
-            navail += ((p & 0xFFu) == cx && ((p >> 8) & 0xFFu) == cy && (p >> 16) != 0u) ? 1 : 0;
-        }
+        for (int k = 0; k < kMaxPkg; ++k) navail += (uint32_t)L.food[ci * kMaxPkg + k] == cell ? 1 : 0;
         int take = -1;
         if (navail > 0) {
             int rank = 0;
             for (int j = 0; j < i; ++j) rank += (L.key[j] == kk) ? 1 : 0;
             if (rank < navail) {
                 for (int k = 0; k < kMaxPkg; ++k) {
-                    uint32_t p = L.food[ci * kMaxPkg + k];
-                    if ((p & 0xFFu) == cx && ((p >> 8) & 0xFFu) == cy && (p >> 16) != 0u) {
+                    if ((uint32_t)L.food[ci * kMaxPkg + k] == cell) {
                         if (rank == 0) { take = ci * kMaxPkg + k; break; }
                         --rank;
                     }
@@ -309,7 +310,7 @@ __device__ void world_step(SimState &S, const ObsTable &cur, WorldLDS &L, uint32
             uint32_t fl = L.flags[i];
             const int take = L.take[i];
             if (take >= 0) {
-                L.food[take] &= 0xFFFFu;   // numFood 1 -> 0
+                L.food[take] &= (uint16_t)0xFFu;   // numFood 1 -> 0
                 atomicAdd(&L.consumed, 1);
                 h = (int32_t)((float)h + 20.0f);
                 fl |= F_ATE;
@@ -403,13 +404,13 @@ __device__ void world_step(SimState &S, const ObsTable &cur, WorldLDS &L, uint32
         const uint64_t m = ballot64(alive);
         if (alive) {
             const size_t d = base + nn + rank_below(m);
-            S.x[d] = L.x[i];
-            S.y[d] = L.y[i];
-            S.rw[d] = L.rw[i];
-            S.rz[d] = L.rz[i];
-            S.species[d] = L.species[i];
+            S.x_out[d] = L.x[i];
+            S.y_out[d] = L.y[i];
+            S.rw_out[d] = L.rw[i];
+            S.rz_out[d] = L.rz[i];
+            S.species_out[d] = L.species[i];
             S.health[d] = L.accum[i];
-            S.obsrow[d] = L.obsrow[i];
+            S.obsrow_out[d] = L.obsrow[i];
             S.sur0[d] = L.sur0[i];
             S.sur1[d] = L.sur1[i];
             S.stats[d] = L.flags[i] & F_STATS;
@@ -417,11 +418,11 @@ __device__ void world_step(SimState &S, const ObsTable &cur, WorldLDS &L, uint32
         }
         nn += __popcll(m);
     }
-    if (lane < kNumChunks) S.food[(size_t)w * kNumChunks + lane] = food_pack(&L.food[lane * kMaxPkg]);
+    if (lane < kNumChunks) S.food_out[(size_t)w * kNumChunks + lane] = food_pack(&L.food[lane * kMaxPkg]);
     wave_sync();
     if (lane < kNumSpecies) S.scount[(size_t)w * kNumSpecies + lane] = L.scount[lane];
     if (lane == 0) {
-        S.n[w] = nn;
+        S.n_out[w] = nn;
         S.ctr[w] = ctr;
         S.cur_food[w] = cur_food;
         if (ovf) S.overflow[w] += ovf;
@@ -553,10 +554,10 @@ __global__ __launch_bounds__(256) void export_rows_kernel(SimState S, ObsTable n
 {
     const uint32_t wv = threadIdx.x >> 6;
     const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t w = blockIdx.x * kWorldsPerBlock + wv;
+    const uint32_t w = uniform(blockIdx.x * kWorldsPerBlock + wv);
     if (w >= S.W) return;
     const size_t base = (size_t)w * S.cap;
-    const int n = S.n[w];
+    const int n = uniform(S.n[w]);
     const int4 rb = reinterpret_cast<const int4 *>(S.row_base)[w];
     const float4 rew = reinterpret_cast<const float4 *>(S.sreward)[w];
     const bool fixed = (S.flags & kFlagRewardFixed) != 0;
@@ -688,12 +689,8 @@ constexpr int kKeyAgents = MB_KEY_AGENTS;     // agents per chunk (key rows)
 constexpr int kKeyStride = 36;                // key row: 32 pixels, finder, pad (16-B rows)
 constexpr int kQueueCap = 128;                // P1 survivors (flushed at >= 64)
 constexpr int kWideCap = 64;                  // wide pairs of one survivor batch
-constexpr int kMaxFood = kFoodCap + 2;        // live packages == currentNumFood <= 30
 constexpr float kWedge = 1.41421356f + 0.05f; // |l| <= |f| + sqrt(2): necessary for |u| < 1
 constexpr float kUEps = 2e-3f;                // root-interval margin in u
-constexpr uint32_t kOrderFood = 1u;           // object order: wall 0, food 1.., agents 64..
-constexpr uint32_t kOrderAgent = 64u;
-constexpr uint32_t kNoKey = 0xFFFFFFFFu;
 
 struct SensorLDS {
     float2 obj[kMaxFood + kMaxCap];           // positions: food, then agents
@@ -706,10 +703,6 @@ struct SensorLDS {
     alignas(16) float u[kSensor];
 };
 
-constexpr float kInLo = 0.0f + 0.2f;          // inner arena rectangle (walls, sim.cpp:157-194)
-constexpr float kInHiX = 128.0f - 0.2f;
-constexpr float kInHiY = 96.0f - 0.2f;
-
 // pinhole offsets (IEEE constant folding == the oracle's runtime division)
 constexpr float u_of(int k)
 {
@@ -719,44 +712,6 @@ constexpr float u_of(int k)
 __constant__ float kURay[kSensor] = {MB_U4(0),  MB_U4(4),  MB_U4(8),  MB_U4(12),
                                      MB_U4(16), MB_U4(20), MB_U4(24), MB_U4(28)};
 #undef MB_U4
-
-__device__ __forceinline__ float max0(float x) { return x > 0.0f ? x : 0.0f; }
-__device__ __forceinline__ float zq(float z) { return __uint_as_float(__float_as_uint(z) & ~0xFFu); }
-__device__ __forceinline__ uint32_t zkey(float z, uint32_t order)
-{
-    return (__float_as_uint(z) & ~0xFFu) | order;
-}
-
-// predicates below use non-short-circuit & | so they compile to VALU selects,
-// not exec-mask branches; the float operations are the oracle's
-__device__ __forceinline__ bool inside_arena(float ox, float oy)
-{
-    return (ox >= kInLo) & (ox <= kInHiX) & (oy >= kInLo) & (oy <= kInHiY);
-}
-
-// wall depth of a ray: exit from the inner rectangle; 0 inside a wall box
-__device__ __forceinline__ float wall_z(float ox, float oy, float dx, float dy)
-{
-    if (!inside_arena(ox, oy)) return 0.0f;
-    float tx = __builtin_inff(), ty = __builtin_inff();
-    if (dx > 0.0f) tx = (kInHiX - ox) / dx;
-    else if (dx < 0.0f) tx = (kInLo - ox) / dx;
-    if (dy > 0.0f) ty = (kInHiY - oy) / dy;
-    else if (dy < 0.0f) ty = (kInLo - oy) / dy;
-    const float t = fmin_std(tx, ty);
-    return t == 0.0f ? 0.0f : t;
-}
-
-// object at view depth z hides the wall iff z * d < (X - o) per axis
-__device__ __forceinline__ bool beats_wall(float ox, float oy, float dx, float dy, float z)
-{
-    const float zx = z * dx, zy = z * dy;
-    const bool bx = ((dx > 0.0f) & (zx < kInHiX - ox)) | ((dx < 0.0f) & (zx > kInLo - ox)) |
-                    (dx == 0.0f);
-    const bool by = ((dy > 0.0f) & (zy < kInHiY - oy)) | ((dy < 0.0f) & (zy > kInLo - oy)) |
-                    (dy == 0.0f);
-    return inside_arena(ox, oy) & bx & by;
-}
 
 // (f, l) of object j in agent i's frame; order of the object
 __device__ __forceinline__ void pair_fl(const SensorLDS &L, int nf, int i, int j, float &f,
@@ -769,34 +724,6 @@ __device__ __forceinline__ void pair_fl(const SensorLDS &L, int nf, int i, int j
     const float vx = p.x - a.x, vy = p.y - a.y;
     f = vx * h.x + vy * h.y;   // along the heading
     l = vx * h.y - vy * h.x;   // along r = (hy, -hx)
-}
-
-__device__ __forceinline__ uint32_t order_of(int nf, int j)
-{
-    return j < nf ? kOrderFood + (uint32_t)j : kOrderAgent + (uint32_t)(j - nf);
-}
-
-// exact predicate of (f, l) on pixel ray k < 32 with offset u; key or kNoKey
-__device__ __forceinline__ uint32_t pixel_key(float f, float l, float u, bool fwdk, uint32_t order)
-{
-    const float A = f * f - 1.0f, B2 = 2.0f * (l * f), C = l * l - 1.0f;
-    const float q = (A * u - B2) * u + C;
-    const float p = f + u * l;
-    const bool hit = (q <= 0.0f) & ((fwdk & (p > 0.0f)) | (!fwdk & (p < 0.0f)));
-    const float z = zq(max0(fwdk ? f - 1.0f : -f - 1.0f));
-    const bool near = f * f + l * l <= 1.0f;
-    const uint32_t key = zkey(near ? 0.0f : z, order);
-    return (hit | near) ? key : kNoKey;
-}
-
-// the finder ray (u = 0)
-__device__ __forceinline__ uint32_t finder_key(float f, float l, uint32_t order)
-{
-    const float C = l * l - 1.0f;
-    const bool hit = (C <= 0.0f) & (f > 0.0f);
-    const bool near = f * f + l * l <= 1.0f;
-    const uint32_t key = zkey(near ? 0.0f : zq(max0(f - 1.0f)), order);
-    return (hit | near) ? key : kNoKey;
 }
 
 // W: wide pairs [0, cnt), two per wave (32 lanes each: rays 0..31, lane 0 of
@@ -884,14 +811,14 @@ __device__ __forceinline__ void run_survivors(SensorLDS &L, int nf, int a0, int 
 struct SensorPrefetch {
     uint64_t food;             // lane < 48: packed chunk record
     float x, y, rw, rz;        // lane < min(cap, 64): agent slot `lane`
-    int32_t sp, row;
+    int32_t sp;
     int n;
 };
 
 __device__ __forceinline__ void sensor_prefetch(const SimState &S, uint32_t w, uint32_t lane,
                                                 SensorPrefetch &p)
 {
-    p.n = S.n[w];
+    p.n = uniform(S.n[w]);
     p.food = lane < kNumChunks ? S.food[(size_t)w * kNumChunks + lane] : 0ull;
     if (lane < S.cap) {   // rows past n are allocated (stale); only [0, n) is staged
         const size_t i = (size_t)w * S.cap + lane;
@@ -900,7 +827,6 @@ __device__ __forceinline__ void sensor_prefetch(const SimState &S, uint32_t w, u
         p.rw = S.rw[i];
         p.rz = S.rz[i];
         p.sp = S.species[i];
-        p.row = S.obsrow[i];
     }
 }
 
@@ -910,7 +836,7 @@ __global__ __launch_bounds__(256) void sensor_kernel(SimState S, ObsTable nxt)
     __shared__ SensorLDS lds[kWorldsPerBlock];
     const uint32_t wv = threadIdx.x >> 6;
     const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t w = blockIdx.x * kWorldsPerBlock + wv;
+    const uint32_t w = uniform(blockIdx.x * kWorldsPerBlock + wv);
     if (w >= S.W) return;
     SensorLDS &L = lds[wv];
     const bool depth = (S.flags & kFlagFixDepth) != 0;
@@ -921,38 +847,13 @@ __global__ __launch_bounds__(256) void sensor_kernel(SimState S, ObsTable nxt)
     SensorPrefetch pf;
     sensor_prefetch(S, w, lane, pf);
     do {
-    const unsigned long long t_start = PROF_NOW();
+    [[maybe_unused]] const unsigned long long t_start = PROF_NOW();
     const size_t base = (size_t)w * S.cap;
     const SensorPrefetch cur = pf;
     const int n = cur.n;
 
     // ---- live food packages in (chunk, package) order -> objects [0, nf) ----
-    int nf;
-    {
-        const uint64_t rec = cur.food;
-        const uint32_t live = (uint32_t)(rec >> 40) & 31u;
-        const int cnt = __popc(live);
-        int off = 0, tot = 0;
-#pragma unroll
-        for (int bt = 0; bt < 3; ++bt) {
-            const uint64_t m = ballot64((cnt >> bt) & 1);
-            off += (int)rank_below(m) << bt;
-            tot += __popcll(m) << bt;
-        }
-        const float bx = (float)((lane % kChunksX) * kChunkW);
-        const float by = (float)((lane / kChunksX) * kChunkW);
-        int s = off;
-#pragma unroll
-        for (int k = 0; k < kMaxPkg; ++k) {
-            if ((live >> k) & 1u) {
-                const uint32_t xy = (uint32_t)(rec >> (8 * k)) & 0xFFu;
-                if (s < kMaxFood)   // live packages == currentNumFood <= 30
-                    L.obj[s] = make_float2((float)(xy & 15u) + bx, (float)(xy >> 4) + by);
-                ++s;
-            }
-        }
-        nf = min(tot, kMaxFood);
-    }
+    const int nf = stage_food(cur.food, lane, L.obj);
     // ---- agents -> objects [nf, nf + n) ----
     if ((int)lane < n) {
         float hx, hy;
@@ -961,17 +862,36 @@ __global__ __launch_bounds__(256) void sensor_kernel(SimState S, ObsTable nxt)
         L.hd[lane] = make_float2(hx, hy);
         L.sp[lane] = (int8_t)cur.sp;
     }
-    // export rows stay in registers: lane s holds slot s (row_lo) and 64 + s (row_hi)
-    const int row_lo = cur.row;
-    int row_hi = 0;
-    if (64 + (int)lane < n) {   // slots past 64: loaded here
+    // export rows (K3a's rule, computed here so the sensor need not wait for
+    // K3a): row_base[w][species] + rank among the world's slots of that
+    // species.  They stay in registers: lane s holds slot s (row_lo) and 64 + s
+    // (row_hi).
+    const int4 rb = reinterpret_cast<const int4 *>(S.row_base)[w];
+    int row_lo, row_hi = 0;
+    int c1, c2, c3, c4;
+    {
+        const int sp = (int)lane < n ? cur.sp : 0;
+        const uint64_t m1 = ballot64(sp == 1), m2 = ballot64(sp == 2);
+        const uint64_t m3 = ballot64(sp == 3), m4 = ballot64(sp == 4);
+        row_lo = sp == 1 ? rb.x + (int)rank_below(m1) : sp == 2 ? rb.y + (int)rank_below(m2)
+               : sp == 3 ? rb.z + (int)rank_below(m3) : rb.w + (int)rank_below(m4);
+        c1 = __popcll(m1); c2 = __popcll(m2); c3 = __popcll(m3); c4 = __popcll(m4);
+    }
+    if (n > 64) {   // slots past 64: loaded here
         const int i = 64 + (int)lane;
-        float hx, hy;
-        heading(S.rw[base + i], S.rz[base + i], hx, hy);
-        L.obj[nf + i] = make_float2(S.x[base + i], S.y[base + i]);
-        L.hd[i] = make_float2(hx, hy);
-        L.sp[i] = (int8_t)S.species[base + i];
-        row_hi = S.obsrow[base + i];
+        int sp = 0;
+        if (i < n) {
+            float hx, hy;
+            heading(S.rw[base + i], S.rz[base + i], hx, hy);
+            L.obj[nf + i] = make_float2(S.x[base + i], S.y[base + i]);
+            L.hd[i] = make_float2(hx, hy);
+            sp = S.species[base + i];
+            L.sp[i] = (int8_t)sp;
+        }
+        const uint64_t m1 = ballot64(sp == 1), m2 = ballot64(sp == 2);
+        const uint64_t m3 = ballot64(sp == 3), m4 = ballot64(sp == 4);
+        row_hi = sp == 1 ? rb.x + c1 + (int)rank_below(m1) : sp == 2 ? rb.y + c2 + (int)rank_below(m2)
+               : sp == 3 ? rb.z + c3 + (int)rank_below(m3) : rb.w + c4 + (int)rank_below(m4);
     }
     if (MB_ABL & 1) continue;
     const int nobj = nf + n;
@@ -1000,7 +920,7 @@ __global__ __launch_bounds__(256) void sensor_kernel(SimState S, ObsTable nxt)
             nq += __popcll(m);
             if (nq >= 64) {
                 wave_sync();
-                const unsigned long long ta = PROF_NOW();
+                [[maybe_unused]] const unsigned long long ta = PROF_NOW();
                 run_survivors(L, nf, a0, nq - 64, 64);
                 PROF_ADD(2, PROF_NOW() - ta);
                 PROF_ADD(5, 64);
@@ -1016,13 +936,13 @@ __global__ __launch_bounds__(256) void sensor_kernel(SimState S, ObsTable nxt)
         }
         if (nq > 0) {
             wave_sync();
-            const unsigned long long ta = PROF_NOW();
+            [[maybe_unused]] const unsigned long long ta = PROF_NOW();
             run_survivors(L, nf, a0, 0, nq);
             PROF_ADD(2, PROF_NOW() - ta);
             PROF_ADD(5, nq);
         }
         wave_sync();
-        const unsigned long long to = PROF_NOW();
+        [[maybe_unused]] const unsigned long long to = PROF_NOW();
         // ---- output: keys vs walls; lane = (agent ci, pixels 4g .. 4g+3) ----
         if (!(MB_ABL & 8)) {
             const int ci = (int)(lane >> 3), g = (int)(lane & 7u);
@@ -1060,11 +980,10 @@ __global__ __launch_bounds__(256) void sensor_kernel(SimState S, ObsTable nxt)
         if ((int)lane < nc) {
             const int i = a0 + (int)lane;
             const float2 p = L.obj[nf + i], h = L.hd[i];
-            const float4 a = make_float4(p.x, p.y, h.x, h.y);
             const uint32_t kv = L.key[lane * kKeyStride + kSensor];
             const uint32_t order = kv & 0xFFu;
-            const bool agent = kv != kNoKey && order >= kOrderAgent &&
-                               beats_wall(a.x, a.y, a.z, a.w, __uint_as_float(kv & ~0xFFu));
+            const bool agent = (kv != kNoKey) & (order >= kOrderAgent) &&
+                               beats_wall(p.x, p.y, h.x, h.y, __uint_as_float(kv & ~0xFFu));
             S.finder[base + i] = agent ? (int32_t)(order - kOrderAgent) : -1;
         }
         wave_sync();
@@ -1146,7 +1065,7 @@ __global__ __launch_bounds__(256) void init_kernel(SimState S)
 {
     const uint32_t wv = threadIdx.x >> 6;
     const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t w = blockIdx.x * kWorldsPerBlock + wv;
+    const uint32_t w = uniform(blockIdx.x * kWorldsPerBlock + wv);
     if (w >= S.W) return;
     const size_t base = (size_t)w * S.cap;
     const uint32_t gw = S.world_offset + w;
@@ -1190,11 +1109,11 @@ __global__ __launch_bounds__(256) void synthetic_actions_kernel(SimState S, ObsT
 {
     const uint32_t wv = threadIdx.x >> 6;
     const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t w = blockIdx.x * kWorldsPerBlock + wv;
+    const uint32_t w = uniform(blockIdx.x * kWorldsPerBlock + wv);
     if (w >= S.W) return;
     const size_t base = (size_t)w * S.cap;
     const uint32_t gw = S.world_offset + w;
-    const int n = S.n[w];
+    const int n = uniform(S.n[w]);
     for (int i = lane; i < n; i += 64) {
         const size_t r = (size_t)S.obsrow[base + i];
         const uint32_t k = threefry2x32(seed, step, gw, (uint32_t)i).x % 6u;
@@ -1217,10 +1136,10 @@ __global__ __launch_bounds__(256) void sensor_index_kernel(SimState S, int32_t *
 {
     const uint32_t wv = threadIdx.x >> 6;
     const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t w = blockIdx.x * kWorldsPerBlock + wv;
+    const uint32_t w = uniform(blockIdx.x * kWorldsPerBlock + wv);
     if (w >= S.W) return;
     const size_t base = (size_t)w * S.cap;
-    const int n = S.n[w], off = S.world_off[w];
+    const int n = uniform(S.n[w]), off = S.world_off[w];
     for (int i = lane; i < n; i += 64) out[off + i] = S.obsrow[base + i];
 }
 

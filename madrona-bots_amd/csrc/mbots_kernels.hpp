@@ -31,8 +31,21 @@ struct SimState {
     uint32_t *totals;               // [0] = N, [1..4] = per-species rows
     int32_t *tiles;                 // [2][ntiles][5] per-tile species/agent counts (K1 -> K2)
     unsigned long long *agent_steps;
+    // K1's output half of the double-buffered columns the sensor reads (the
+    // sensor of step t runs beside step t+1's K1; swap_state after each K1)
+    float *x_out, *y_out, *rw_out, *rz_out;
+    int32_t *species_out, *obsrow_out, *n_out;
+    uint64_t *food_out;
     uint32_t W, cap, A, world_offset, flags, seed, ntiles;
 };
+
+inline void swap_state(SimState &S)
+{
+    auto sw = [](auto &a, auto &b) { auto t = a; a = b; b = t; };
+    sw(S.x, S.x_out); sw(S.y, S.y_out); sw(S.rw, S.rw_out); sw(S.rz, S.rz_out);
+    sw(S.species, S.species_out); sw(S.obsrow, S.obsrow_out); sw(S.n, S.n_out);
+    sw(S.food, S.food_out);
+}
 
 // One half of the double-buffered species-major observation table
 // (AgentObservationArchetype, types.hpp:228-252, + raycast output columns).

@@ -72,8 +72,10 @@ struct mbots_handle {
     uint32_t *h_totals = nullptr;     // pinned mirror of S.totals
     hipEvent_t ev_totals = nullptr;
     hipStream_t aux = nullptr;        // internal stream: K4 move next to the K3b sensor
-    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-    bool sensor_pending = false;      // K3b still running on aux (ev_join)
+    hipEvent_t ev_fork = nullptr;
+    hipEvent_t ev_join[2] = {nullptr, nullptr};   // K3b of alternate steps done (aux)
+    int last_join = -1;               // ev_join of the latest K3b, -1: none pending
+    uint64_t steps = 0;               // steps run
     hipStream_t last_stream = nullptr;
     bool timing = false;
     std::vector<TimedPair> pending;
@@ -169,6 +171,14 @@ size_t layout(mbots_handle *h, Arena &a)
     S.ntiles = scan_tiles((uint32_t)W);
     S.tiles = a.take<int32_t>((size_t)2 * S.ntiles * 5);
     S.agent_steps = a.take<unsigned long long>(1);
+    S.x_out = a.take<float>(rows);
+    S.y_out = a.take<float>(rows);
+    S.rw_out = a.take<float>(rows);
+    S.rz_out = a.take<float>(rows);
+    S.species_out = a.take<int32_t>(rows);
+    S.obsrow_out = a.take<int32_t>(rows);
+    S.n_out = a.take<int32_t>(W);
+    S.food_out = a.take<uint64_t>(W * kNumChunks);
     fill_table(h->T[0], a, rows);
     fill_table(h->T[1], a, rows);
     h->done_zeros = a.take<int32_t>(rows);
@@ -182,7 +192,7 @@ hipStream_t as_stream(void *s) { return reinterpret_cast<hipStream_t>(s); }
 // make the caller's stream (the one step() ran on) wait for the sensor rows
 int wait_sensor(mbots_handle *h)
 {
-    if (h->sensor_pending) HIP_TRY(hipStreamWaitEvent(h->last_stream, h->ev_join, 0));
+    if (h->last_join >= 0) HIP_TRY(hipStreamWaitEvent(h->last_stream, h->ev_join[h->last_join], 0));
     return MBOTS_OK;
 }
 
@@ -261,7 +271,8 @@ int mbots_create(const mbots_config *cfg_in, mbots_handle **out)
           "hipHostMalloc");
     check(hipEventCreateWithFlags(&h->ev_totals, hipEventDisableTiming), "hipEventCreate");
     check(hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming), "hipEventCreate");
-    check(hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming), "hipEventCreate");
+    check(hipEventCreateWithFlags(&h->ev_join[0], hipEventDisableTiming), "hipEventCreate");
+    check(hipEventCreateWithFlags(&h->ev_join[1], hipEventDisableTiming), "hipEventCreate");
     check(hipStreamCreateWithFlags(&h->aux, hipStreamNonBlocking), "hipStreamCreate");
     hipStream_t st = nullptr;
     check(hipMemsetAsync(h->arena.base, 0, bytes, st), "hipMemsetAsync");
@@ -295,7 +306,7 @@ int mbots_destroy(mbots_handle *h)
     for (auto e : h->pool) (void)hipEventDestroy(e);
     if (h->ev_totals) (void)hipEventDestroy(h->ev_totals);
     if (h->ev_fork) (void)hipEventDestroy(h->ev_fork);
-    if (h->ev_join) (void)hipEventDestroy(h->ev_join);
+    for (auto e : h->ev_join) if (e) (void)hipEventDestroy(e);
     if (h->aux) (void)hipStreamDestroy(h->aux);
     if (h->h_totals) (void)hipHostFree(h->h_totals);
     if (h->arena.base) (void)hipFree(h->arena.base);
@@ -313,36 +324,42 @@ int mbots_step(mbots_handle *h, void *stream)
     const mbots::ObsTable &nxt = h->T[h->tb ^ 1];
     int rc;
     const int par = h->parity;
-    // the previous step's sensor (aux) wrote the finder slots K1 reads and the
-    // semantic rows K4 moves into the prev-sensor column
-    if (h->sensor_pending) HIP_TRY(hipStreamWaitEvent(st, h->ev_join, 0));
+    // K1 reads the finder slots the previous step's sensor wrote, and writes the
+    // state half that sensor read; the halves swap after K1.
+    if (h->last_join >= 0) HIP_TRY(hipStreamWaitEvent(st, h->ev_join[h->last_join], 0));
     if ((rc = timed(h, MBOTS_TK_WORLD_STEP, st,
                     [&] { return mbots::launch_world_step(h->S, cur, par, st); })))
         return rc;
+    mbots::swap_state(h->S);
     if ((rc = timed(h, MBOTS_TK_SCAN, st, [&] { return mbots::launch_scan(h->S, par, st); }))) return rc;
+#ifdef MB_NO_FORK
     if ((rc = timed(h, MBOTS_TK_EXPORT, st,
                     [&] { return mbots::launch_export_rows(h->S, nxt, 0, st); })))
         return rc;
-#ifdef MB_NO_FORK
     if ((rc = timed(h, MBOTS_TK_MOVE, st, [&] { return mbots::launch_move(h->S, cur, nxt, st); })))
         return rc;
     if ((rc = timed(h, MBOTS_TK_SENSOR, st, [&] { return mbots::launch_sensor(h->S, nxt, st); })))
         return rc;
-    h->sensor_pending = false;
 #else
-    // fork: K3b sensor (VALU-bound) on the aux stream; the caller's stream goes
-    // on with K4 move and whatever follows (shift_observations, the learner's
-    // action writes) -- none of it reads the sensor output.  The next step and
-    // the semantic/depth accessors wait for ev_join.
+    // fork after K2: the K3b sensor (VALU-bound; it derives the export rows from
+    // K2's row_base itself) runs on the aux stream while this stream goes on
+    // with K3a export, K4 move, shift_observations and the learner's action
+    // writes -- none of which reads the sensor rows or the finder slots.  The
+    // next step's K1 and the semantic/depth accessors wait for ev_join.
+    const int jcur = h->last_join == 0 ? 1 : 0;
     HIP_TRY(hipEventRecord(h->ev_fork, st));
     HIP_TRY(hipStreamWaitEvent(h->aux, h->ev_fork, 0));
     if ((rc = timed(h, MBOTS_TK_SENSOR, h->aux, [&] { return mbots::launch_sensor(h->S, nxt, h->aux); })))
         return rc;
-    HIP_TRY(hipEventRecord(h->ev_join, h->aux));
-    h->sensor_pending = true;
+    HIP_TRY(hipEventRecord(h->ev_join[jcur], h->aux));
+    h->last_join = jcur;
+    if ((rc = timed(h, MBOTS_TK_EXPORT, st,
+                    [&] { return mbots::launch_export_rows(h->S, nxt, 0, st); })))
+        return rc;
     if ((rc = timed(h, MBOTS_TK_MOVE, st, [&] { return mbots::launch_move(h->S, cur, nxt, st); })))
         return rc;
 #endif
+    ++h->steps;
     h->parity ^= 1;
     h->tb ^= 1;
     return record_totals(h, st);
