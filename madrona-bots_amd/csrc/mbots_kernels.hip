@@ -62,7 +62,7 @@ __device__ __forceinline__ uint64_t food_pack(const uint16_t *pk)
 // ---------------------------------------------------------------------------
 struct WorldLDS {
     float x[kMaxCap], y[kMaxCap], rw[kMaxCap], rz[kMaxCap];
-    int32_t accum[kMaxCap], obsrow[kMaxCap];
+    int32_t accum[kMaxCap];
     int8_t species[kMaxCap], finder[kMaxCap];
     uint8_t flags[kMaxCap];
     // healthSync's cell keys / package takes (slots < n0) share storage with the
@@ -105,7 +105,6 @@ __device__ __forceinline__ void init_slot(WorldLDS &L, int s, float x, float y, 
     L.species[s] = (int8_t)sp;
     L.accum[s] = h;
     L.finder[s] = -1;
-    L.obsrow[s] = -1;
     L.flags[s] = (uint8_t)F_ALIVE;
     L.sur0[s] = 0.0f;
     L.sur1[s] = 0.0f;
@@ -120,7 +119,7 @@ __device__ __forceinline__ void init_slot(WorldLDS &L, int s, float x, float y, 
 __device__ void world_step(SimState &S, const ObsTable &cur, WorldLDS &L, uint32_t w,
                            uint32_t lane);
 
-__global__ __launch_bounds__(256) void world_step_kernel(SimState S, ObsTable cur, int parity)
+__global__ __launch_bounds__(256, 8) void world_step_kernel(SimState S, ObsTable cur, int parity)
 {
     __shared__ WorldLDS lds[kWorldsPerBlock];
     __shared__ int32_t blk[kWorldsPerBlock][5];
@@ -158,9 +157,14 @@ __device__ void world_step(SimState &S, const ObsTable &cur, WorldLDS &L, uint32
 
     // ---- stage the world in LDS; slot `lane`'s action row is fetched now and
     // consumed after addFood (its latency hides behind that serial phase) ----
+    // The old export rows stay in registers (slot lane: row_lo, 64 + lane:
+    // row_hi): only the slot's own lane reads them (action fetch, compaction).
     int2 pa0 = make_int2(0, 0), pa1 = pa0, pa2 = pa0;
+    int32_t row_lo = -1, row_hi = -1;
     for (int i = lane; i < n0; i += 64) {
         const int32_t row = S.obsrow[base + i];
+        if (i < 64) row_lo = row;
+        else row_hi = row;
         if (i < 64 && row >= 0) {
             const int2 *ap = reinterpret_cast<const int2 *>(cur.action + (size_t)row * 6);
             pa0 = ap[0]; pa1 = ap[1]; pa2 = ap[2];
@@ -172,7 +176,6 @@ __device__ void world_step(SimState &S, const ObsTable &cur, WorldLDS &L, uint32
         L.species[i] = (int8_t)S.species[base + i];
         L.accum[i] = S.health[base + i];
         L.finder[i] = (int8_t)S.finder[base + i];
-        L.obsrow[i] = row;
         L.flags[i] = (uint8_t)F_ALIVE;
     }
     if (lane < kNumChunks) food_unpack(S.food[(size_t)w * kNumChunks + lane], &L.food[lane * kMaxPkg]);
@@ -224,7 +227,7 @@ __device__ void world_step(SimState &S, const ObsTable &cur, WorldLDS &L, uint32
     // ---- actionSystem (sim.cpp:419-502) ----
     for (int i = lane; i < n0; i += 64) {
         int2 a0 = pa0, a1 = pa1, a2 = pa2;
-        const int32_t row = L.obsrow[i];
+        const int32_t row = i < 64 ? row_lo : row_hi;
         if (i >= 64 && row >= 0) {
             const int2 *ap = reinterpret_cast<const int2 *>(cur.action + (size_t)row * 6);
             a0 = ap[0]; a1 = ap[1]; a2 = ap[2];
@@ -410,7 +413,7 @@ __device__ void world_step(SimState &S, const ObsTable &cur, WorldLDS &L, uint32
             S.rz_out[d] = L.rz[i];
             S.species_out[d] = L.species[i];
             S.health[d] = L.accum[i];
-            S.obsrow_out[d] = L.obsrow[i];
+            S.obsrow_out[d] = i < n0 ? (b == 0 ? row_lo : row_hi) : -1;   // newborns: no row
             S.sur0[d] = L.sur0[i];
             S.sur1[d] = L.sur1[i];
             S.stats[d] = L.flags[i] & F_STATS;
