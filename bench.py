@@ -10,6 +10,12 @@ BASELINE config 3).  Rank 0 prints one JSON line.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--worlds WPG]
     torchrun --nproc-per-node N bench.py --gpus N ...
+
+--gather (BASELINE config 5): every step also builds the learner observation
+rows (fused construct_obs kernel) and gathers them with the rewards to rank 0
+over RCCL (madrona-bots_amd/harness/gather.py); reported as "config5".
+A secondary line at 4096 worlds/GPU (BASELINE config 2; the metric names both
+sizes) is measured after the main one unless --no-secondary.
 """
 import argparse
 import json
@@ -19,6 +25,7 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "madrona-bots_amd"))
+sys.path.insert(0, os.path.join(ROOT, "madrona-bots_amd", "harness"))
 
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
@@ -75,6 +82,37 @@ def cpu_baseline(worlds_sample, target_s):
                       f"{dt:.1f} s"}
 
 
+def secondary_run(W, args, rank, world_size, dev, distributed):
+    """BASELINE config 2 size (4096 worlds/GPU), same step, same timing rule."""
+    import madrona_bots as mb
+    m = mb.SimManager(dev.index, W, SEED, AGENTS_PER_WORLD, world_offset=rank * W)
+    m.write_synthetic_actions(ACTION_SEED, 0)
+    for t in range(args.warmup):
+        m.step(); m.shift_observations(); m.write_synthetic_actions(ACTION_SEED, t + 1)
+    torch.cuda.synchronize()
+    s0 = m.agent_steps()
+    if distributed:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for t in range(args.warmup, args.warmup + args.steps):
+        m.step(); m.shift_observations(); m.write_synthetic_actions(ACTION_SEED, t + 1)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    st = torch.tensor([el, float(m.agent_steps() - s0)], dtype=torch.float64, device=dev)
+    if distributed:
+        dist.barrier()
+        tm = st[0:1].clone(); dist.all_reduce(tm, op=dist.ReduceOp.MAX)
+        tot = st[1:2].clone(); dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+        el, total = float(tm.item()), float(tot.item())
+    else:
+        total = float(st[1].item())
+    del m
+    return {"worlds_per_gpu": W, "value": total / el, "unit": "agent-steps/s",
+            "ms_per_step": el / args.steps * 1e3, "n_gpus": world_size,
+            "note": "BASELINE config 2 size, same step/timing as the main line"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -85,6 +123,10 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true")
+    ap.add_argument("--gather", action="store_true",
+                    help="config 5: construct_obs + RCCL gather of obs/reward rows to rank 0")
+    ap.add_argument("--no-secondary", action="store_true",
+                    help="skip the 4096-worlds/GPU secondary measurement")
     args = ap.parse_args()
 
     world_size = int(os.environ.get("WORLD_SIZE", "1"))
@@ -102,8 +144,21 @@ def main():
     W = args.worlds
     mgr = mb.SimManager(local_rank, W, SEED, AGENTS_PER_WORLD, world_offset=rank * W)
 
+    gather_s = [0.0]
+
+    def learner_gather():
+        # the learner's read of this step's rows (learn/env.py:58-70) moved to rank 0
+        import gather
+        obs = mgr.construct_obs(False)
+        rew = mgr.reward_tensor(False).to_torch()
+        cnt = gather.species_rows(mgr.species_count_tensor().to_torch())
+        if distributed:
+            gather.gather_rollout({"obs": obs, "reward": rew}, cnt, dst=0)
+
     def one_step(t):
         mgr.step()
+        if args.gather:
+            learner_gather()
         mgr.shift_observations()
         mgr.write_synthetic_actions(ACTION_SEED, t + 1)
 
@@ -127,6 +182,10 @@ def main():
     for k, t in enumerate(range(args.warmup, args.warmup + args.steps)):
         ev[k][0].record()
         mgr.step()
+        if args.gather:
+            g0 = time.perf_counter()
+            learner_gather()
+            gather_s[0] += time.perf_counter() - g0
         mgr.shift_observations()
         ev[k][1].record()
         mgr.write_synthetic_actions(ACTION_SEED, t + 1)
@@ -139,6 +198,9 @@ def main():
 
     agent_steps = mgr.agent_steps() - steps_before
     ktimes = mgr.kernel_times() if not args.no_kernel_timing else {}
+    secondary = None
+    if not args.no_secondary and W != 4096:
+        secondary = secondary_run(4096, args, rank, world_size, dev, distributed)
     stats = torch.tensor([elapsed, float(agent_steps)], dtype=torch.float64, device=dev)
     if distributed:
         tmax = stats[0:1].clone()
@@ -189,6 +251,13 @@ def main():
         if ktimes:
             per = {k: (ms / n if n else 0.0) for k, (ms, n) in ktimes.items()}
             out["kernel_ms"] = {k: round(v, 5) for k, v in per.items() if v}
+        if args.gather:
+            out["config5"] = {"what": "step + fused construct_obs + RCCL gather of obs [N,69] f32 "
+                                      "and reward rows to rank 0 (harness/gather.py) + shift",
+                              "host_gather_ms_per_step": gather_s[0] / args.steps * 1e3,
+                              "gathered_bytes_per_step": total_agent_steps / args.steps * 70 * 4}
+        if secondary:
+            out["secondary"] = secondary
         if not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args.cpu_worlds, args.cpu_seconds)
         print(json.dumps(out), flush=True)

@@ -117,6 +117,14 @@ int mbots_set_action(mbots_handle *h, uint32_t row, const int32_t action[6]);
 /* Manager::agentOffsetForWorld (mgr.cpp:342-345) */
 int mbots_agent_offset_for_world(mbots_handle *h, uint32_t world, uint32_t *out);
 
+/* Learner observation rows (learn/util.py:14-29 construct_obs over every
+ * species at once): out (device, >= out_rows x 69 f32, row-major) receives rows
+ * [0, min(N, out_rows)) of [depth 32 | health 1 | position 2 | semantic 32 |
+ * surrounding 2], exactly torch.cat's promotion of the exported views
+ * (prev != 0: the Prev* views).  Launched on `stream` after the sensor rows. */
+int mbots_construct_obs(mbots_handle *h, int32_t prev, float *out, uint64_t out_rows,
+                        void *stream);
+
 /* Build utilities (benchmark / test harness, not reference API):
  * identity-keyed synthetic action stream: one-hot(threefry(seed,step |
  * global_world, slot) % 6) written into the Action column of every live agent;

@@ -1027,6 +1027,37 @@ extern "C" __attribute__((visibility("default"))) int mbots_debug_sensor_prof(un
 #endif
 
 // ---------------------------------------------------------------------------
+// Learner observation rows (learn/util.py:14-29 construct_obs):
+// out[r] = [depth 32 | health 1 | position 2 | semantic 32 | surrounding 2] as
+// f32 -- torch.cat's promotion of the five exported views: depth bytes as
+// uint8 (the semantic buffer when depth aliases it, B.1), health as the f32
+// reinterpretation of its int32 bits (B.2), semantic bytes as int8.  All N rows
+// (every species, species-major) in one pass; thread = one float of the output.
+// ---------------------------------------------------------------------------
+constexpr int kObsDim = 69;
+__global__ __launch_bounds__(256) void construct_obs_kernel(const uint32_t *totals,
+                                                            const uint8_t *depth,
+                                                            const int8_t *sem,
+                                                            const int32_t *health,
+                                                            const float *pos, const float *sur,
+                                                            float *out, uint32_t out_rows)
+{
+    const uint32_t N = min(totals[0], out_rows);
+    const size_t items = (size_t)N * kObsDim;
+    const size_t stride = (size_t)gridDim.x * blockDim.x;
+    for (size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x; idx < items; idx += stride) {
+        const uint32_t r = (uint32_t)(idx / kObsDim), c = (uint32_t)(idx - (size_t)r * kObsDim);
+        float v;
+        if (c < 32) v = (float)depth[(size_t)r * kSensor + c];
+        else if (c == 32) v = __int_as_float(health[r]);
+        else if (c < 35) v = pos[(size_t)r * 2 + (c - 33)];
+        else if (c < 67) v = (float)sem[(size_t)r * kSensor + (c - 35)];
+        else v = sur[(size_t)r * 2 + (c - 67)];
+        out[idx] = v;
+    }
+}
+
+// ---------------------------------------------------------------------------
 // K5: shiftObservationsSystem + shiftHiddenState (sim.cpp:1002-1048): Prev* <-
 // current for rows [0, N).  Each column is a contiguous byte range, so the copy
 // is one grid-stride stream of 16-byte granules over the concatenation of the
@@ -1216,6 +1247,17 @@ hipError_t launch_synthetic_actions(const SimState &S, const ObsTable &t, uint32
 {
     hipLaunchKernelGGL(synthetic_actions_kernel, dim3(world_blocks(S.W)), dim3(256), 0, st, S, t,
                        seed, step, write_hidden);
+    return hipGetLastError();
+}
+hipError_t launch_construct_obs(const SimState &S, const ObsTable &t, int prev, float *out,
+                                uint32_t out_rows, hipStream_t st)
+{
+    const bool fixd = (S.flags & kFlagFixDepth) != 0;
+    const int8_t *sem = prev ? t.psem : t.sem;
+    const uint8_t *depth = fixd ? (prev ? t.pdepth : t.depth) : reinterpret_cast<const uint8_t *>(sem);
+    hipLaunchKernelGGL(construct_obs_kernel, dim3(4096), dim3(256), 0, st, S.totals, depth, sem,
+                       prev ? t.phealth : t.health, prev ? t.ppos : t.pos, prev ? t.psur : t.sur,
+                       out, out_rows);
     return hipGetLastError();
 }
 hipError_t launch_sensor_index(const SimState &S, int32_t *out, hipStream_t st)

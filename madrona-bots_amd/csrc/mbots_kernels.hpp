@@ -68,5 +68,7 @@ hipError_t launch_shift(const SimState &S, const ObsTable &t, hipStream_t st);
 hipError_t launch_synthetic_actions(const SimState &S, const ObsTable &t, uint32_t seed,
                                     uint32_t step, int write_hidden, hipStream_t st);
 hipError_t launch_sensor_index(const SimState &S, int32_t *out, hipStream_t st);
+hipError_t launch_construct_obs(const SimState &S, const ObsTable &t, int prev, float *out,
+                                uint32_t out_rows, hipStream_t st);
 
 }  // namespace mbots

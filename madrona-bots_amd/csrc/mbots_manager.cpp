@@ -479,6 +479,19 @@ int mbots_write_synthetic_actions(mbots_handle *h, uint32_t seed, uint32_t step,
     });
 }
 
+int mbots_construct_obs(mbots_handle *h, int32_t prev, float *out, uint64_t out_rows, void *stream)
+{
+    if (!h || !out) return fail(MBOTS_E_INVALID, "null argument");
+    if (out_rows > 0xFFFFFFFFull) return fail(MBOTS_E_INVALID, "out_rows too large");
+    HIP_TRY(hipSetDevice(h->device));
+    hipStream_t st = as_stream(stream);
+    h->last_stream = st;
+    int rc;
+    if (!prev && (rc = wait_sensor(h))) return rc;   // current semantic rows come from K3b
+    HIP_TRY(mbots::launch_construct_obs(h->S, h->T[h->tb], prev, out, (uint32_t)out_rows, st));
+    return MBOTS_OK;
+}
+
 int mbots_agent_steps(mbots_handle *h, uint64_t *out)
 {
     if (!h || !out) return fail(MBOTS_E_INVALID, "null argument");

@@ -1,0 +1,56 @@
+"""Rollout gather to the learner rank (BASELINE config 5).
+
+Each rank steps its own world shard ([r*W, (r+1)*W), no collective on the
+step) and exports species-major rows.  The learner (PPO, learn/train.py --
+out of scope) runs on one rank; this moves the per-species row tensors it
+consumes there:
+
+  1. all_gather of the per-rank species row counts (4 x int64),
+  2. one gather per tensor of the rows padded to the largest rank
+     (torch.distributed.gather: RCCL send/recv over xGMI with the nccl
+     backend -- each peer has a direct link to the learner -- gloo on CPU),
+  3. on the learner rank, per species s the concatenation over ranks of
+     rank r's species-s rows: the global (species, world, slot) order, i.e.
+     exactly the table one device holding every world would export.
+
+    out = gather_rollout({"obs": obs, "reward": rew}, species_rows, dst=0)
+"""
+import torch
+import torch.distributed as dist
+
+
+def species_rows(counts):
+    """Per-species row counts of this rank from species_count_tensor() [W, 4]."""
+    return counts.sum(dim=0).to(torch.int64)
+
+
+def gather_rollout(tensors, rows_per_species, dst=0, group=None):
+    """tensors: name -> [N_r, ...] species-major rows of this rank (same N_r);
+    rows_per_species: int64 [4] summing to N_r.  Returns name -> [sum N_r, ...]
+    in global species-major order on rank dst, None elsewhere."""
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    dev = next(iter(tensors.values())).device
+    cnt = rows_per_species.to(device=dev, dtype=torch.int64).reshape(4)
+    all_cnt = [torch.zeros_like(cnt) for _ in range(world)]
+    dist.all_gather(all_cnt, cnt, group=group)
+    all_cnt = torch.stack(all_cnt).cpu()              # [world, 4]
+    totals = all_cnt.sum(dim=1)
+    n_max = int(totals.max())
+    out = {} if rank == dst else None
+    for name, t in tensors.items():
+        n = int(totals[rank])
+        if t.shape[0] != n:
+            raise ValueError(f"{name}: {t.shape[0]} rows, species counts sum to {n}")
+        pad = torch.zeros((n_max,) + tuple(t.shape[1:]), dtype=t.dtype, device=dev)
+        pad[:n] = t
+        bufs = [torch.empty_like(pad) for _ in range(world)] if rank == dst else None
+        dist.gather(pad, bufs, dst=dst, group=group)
+        if rank == dst:
+            parts = []
+            for s in range(4):
+                for r in range(world):
+                    a = int(all_cnt[r, :s].sum())
+                    parts.append(bufs[r][a:a + int(all_cnt[r, s])])
+            out[name] = torch.cat(parts)
+    return out

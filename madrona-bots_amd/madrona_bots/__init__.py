@@ -55,6 +55,7 @@ def _load():
         "mbots_step": [vp, vp],
         "mbots_shift_observations": [vp, vp],
         "mbots_num_agents": [vp, P(u32)],
+        "mbots_construct_obs": [vp, i32, vp, ctypes.c_uint64, vp],
         "mbots_export": [vp, i32, P(_CTensor)],
         "mbots_set_action": [vp, u32, P(i32)],
         "mbots_agent_offset_for_world": [vp, u32, P(u32)],
@@ -98,6 +99,7 @@ FLAG_REWARD_FIXED = 0x1
 FLAG_FIX_DEPTH_ALIAS = 0x2
 
 # TK_* indices of mbots_kernel_times
+OBS_DIM = 69   # learn/env.py:19
 KERNELS = ("world_step", "scan", "export", "sensor", "shift", "actions", "move")
 
 
@@ -236,6 +238,24 @@ class SimManager:
         v = ctypes.c_uint32()
         _check(_lib.mbots_num_agents(self._h, ctypes.byref(v)))
         return v.value
+
+    def construct_obs(self, is_prev=False, out=None):
+        """learn/util.py construct_obs over all N rows (every species, species-
+        major) in one fused kernel: float32 [N, 69] = depth | health | position |
+        semantic | surrounding, bit-identical to the torch.cat of the views.
+        Slice [start:end] per species with species_count_tensor()."""
+        import torch
+        n = self.num_agents()
+        if out is None:
+            out = torch.empty((n, OBS_DIM), dtype=torch.float32,
+                              device=torch.device("cuda", self.gpu_id))
+        if out.dtype != torch.float32 or not out.is_cuda or not out.is_contiguous() \
+                or out.dim() != 2 or out.shape[1] != OBS_DIM or out.shape[0] < n:
+            raise ValueError(f"out must be a contiguous CUDA float32 [>= {n}, {OBS_DIM}] tensor")
+        _check(_lib.mbots_construct_obs(self._h, 1 if is_prev else 0,
+                                        ctypes.c_void_p(out.data_ptr()), out.shape[0],
+                                        self._stream()))
+        return out[:n]
 
     def write_synthetic_actions(self, seed, step, write_hidden=False):
         _check(_lib.mbots_write_synthetic_actions(self._h, int(seed) & 0xFFFFFFFF,

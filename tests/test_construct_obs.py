@@ -1,0 +1,49 @@
+"""Fused learner observation rows (SimManager.construct_obs, the HIP
+construct_obs kernel) against learn/util.py:14-29's torch.cat of the exported
+views (madrona-bots_amd/harness/rollout.py construct_obs), bit for bit."""
+import os
+import sys
+
+import pytest
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "madrona-bots_amd", "harness"))
+
+import rollout  # noqa: E402
+
+
+def _bits(t):
+    return t.contiguous().view(torch.int32)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fix_depth", [False, True])
+def test_fused_obs_equals_torch_cat(fix_depth):
+    import madrona_bots as mb
+    sim = mb.SimManager(0, 512, 69, 32, fix_depth_alias=fix_depth)
+    sim.write_synthetic_actions(1234, 0)
+    for t in range(6):
+        sim.step()
+        for prev in (False, True):
+            fused = sim.construct_obs(prev)
+            assert fused.shape == (sim.num_agents(), rollout.OBS_DIM)
+            for s, e in rollout.species_offsets(sim):
+                ref = rollout.construct_obs(sim, s, e, prev=prev)
+                assert torch.equal(_bits(fused[s:e]), _bits(ref)), (t, prev, s, e)
+        sim.shift_observations()
+        sim.write_synthetic_actions(1234, t + 1)
+
+
+@pytest.mark.gpu
+def test_fused_obs_out_buffer():
+    import madrona_bots as mb
+    sim = mb.SimManager(0, 64, 7, 16)
+    sim.step()
+    n = sim.num_agents()
+    buf = torch.full((n + 5, rollout.OBS_DIM), -7.0, device="cuda")
+    out = sim.construct_obs(False, out=buf)
+    assert out.data_ptr() == buf.data_ptr() and out.shape[0] == n
+    assert torch.all(buf[n:] == -7.0)
+    with pytest.raises(ValueError):
+        sim.construct_obs(False, out=torch.empty((n - 1, rollout.OBS_DIM), device="cuda"))

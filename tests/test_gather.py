@@ -1,0 +1,73 @@
+"""Rollout gather to the learner rank (harness/gather.py, BASELINE config 5)
+over gloo with 2 CPU ranks: rank r steps worlds [r*W, (r+1)*W) through the
+oracle adapter; the gathered observation / action / health rows on rank 0 must
+equal the single-process table of all 2W worlds (global species-major order).
+Rewards are excluded: the faithful B.3 reward of species 4 in a shard's last
+world reads 0 per shard."""
+import os
+import sys
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HARNESS = os.path.join(ROOT, "madrona-bots_amd", "harness")
+W, STEPS, SEED = 6, 4, 69
+
+
+def _rows(sim):
+    import rollout
+    obs = torch.cat([rollout.construct_obs(sim, s, e) for s, e in rollout.species_offsets(sim)])
+    return {"obs": obs, "action": sim.action_tensor(False).to_torch().clone(),
+            "health": sim.health_tensor(False).to_torch().clone()}
+
+
+def _run(sim, steps):
+    for t in range(steps):
+        sim._s.write_synthetic_actions(1234, t)
+        sim.step()
+        sim.shift_observations()
+
+
+def _worker(rank, world, port, q):
+    sys.path[:0] = [HARNESS, os.path.join(ROOT, "tests"), os.path.join(ROOT, "oracle")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from oracle_adapter import OracleSimManager
+        import gather
+        sim = OracleSimManager(0, W, SEED, 32, world_offset=rank * W)
+        _run(sim, STEPS)
+        rows = _rows(sim)
+        cnt = gather.species_rows(sim.species_count_tensor().to_torch())
+        out = gather.gather_rollout(rows, cnt, dst=0)
+        if rank == 0:
+            full = OracleSimManager(0, world * W, SEED, 32)
+            _run(full, STEPS)
+            ref = _rows(full)
+            ok = {k: torch.equal(out[k].view(torch.int32), ref[k].contiguous().view(torch.int32))
+                  for k in ref}
+            q.put(ok)
+        else:
+            assert out is None
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gather_two_shards_equals_one():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=240)
+        assert p.exitcode == 0
+    ok = q.get(timeout=5)
+    assert all(ok.values()), ok
