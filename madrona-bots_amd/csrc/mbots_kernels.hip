@@ -907,8 +907,10 @@ __global__ __launch_bounds__(256) void sensor_kernel(SimState S, ObsTable nxt)
         wave_sync();
         // ---- P1: wedge pre-cull of the chunk's (agent, object) pairs ----
         int nq = 0;
-        int ic = 0, j = (int)lane;
-        while (j >= nobj) { j -= nobj; ++ic; }
+        // flattened pair p = ic * nobj + j; advancing p by 64 = (q, r) with
+        // 64 = q * nobj + r (wave-uniform), then one conditional carry
+        const int adv_q = 64 / nobj, adv_r = 64 - adv_q * nobj;
+        int ic = (int)lane / nobj, j = (int)lane - ic * nobj;
         const int npairs = nc * nobj;
         for (int qb = 0; qb < npairs; qb += 64) {
             bool keep = false;
@@ -930,12 +932,11 @@ __global__ __launch_bounds__(256) void sensor_kernel(SimState S, ObsTable nxt)
                 nq -= 64;
             }
             // advance the flattened (agent, object) index by 64
-            j += 64;
-            if (nobj >= 64) {
-                if (j >= nobj) { j -= nobj; ++ic; }
-            } else {
-                while (j >= nobj) { j -= nobj; ++ic; }
-            }
+            j += adv_r;
+            ic += adv_q;
+            const bool carry = j >= nobj;
+            j -= carry ? nobj : 0;
+            ic += carry ? 1 : 0;
         }
         if (nq > 0) {
             wave_sync();
