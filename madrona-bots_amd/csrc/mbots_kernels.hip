@@ -834,12 +834,16 @@ __device__ __forceinline__ void sensor_prefetch(const SimState &S, uint32_t w, u
 }
 
 // one wave per world, 4 worlds per block
-__global__ __launch_bounds__(256) void sensor_kernel(SimState S, ObsTable nxt)
+#ifndef MB_SENSOR_WPB
+#define MB_SENSOR_WPB 4
+#endif
+constexpr int kSensorWorlds = MB_SENSOR_WPB;   // worlds (waves) per sensor block
+__global__ __launch_bounds__(64 * kSensorWorlds) void sensor_kernel(SimState S, ObsTable nxt)
 {
-    __shared__ SensorLDS lds[kWorldsPerBlock];
+    __shared__ SensorLDS lds[kSensorWorlds];
     const uint32_t wv = threadIdx.x >> 6;
     const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t w = uniform(blockIdx.x * kWorldsPerBlock + wv);
+    const uint32_t w = uniform(blockIdx.x * kSensorWorlds + wv);
     if (w >= S.W) return;
     SensorLDS &L = lds[wv];
     const bool depth = (S.flags & kFlagFixDepth) != 0;
@@ -1235,7 +1239,8 @@ hipError_t launch_move(const SimState &S, const ObsTable &cur, const ObsTable &n
 }
 hipError_t launch_sensor(const SimState &S, const ObsTable &nxt, hipStream_t st)
 {
-    hipLaunchKernelGGL(sensor_kernel, dim3(world_blocks(S.W)), dim3(256), 0, st, S, nxt);
+    hipLaunchKernelGGL(sensor_kernel, dim3((S.W + kSensorWorlds - 1) / kSensorWorlds),
+                       dim3(64 * kSensorWorlds), 0, st, S, nxt);
     return hipGetLastError();
 }
 hipError_t launch_shift(const SimState &S, const ObsTable &t, hipStream_t st)

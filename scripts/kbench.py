@@ -13,7 +13,11 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--worlds", type=int, default=65536)
 ap.add_argument("--steps", type=int, default=40)
 ap.add_argument("--warmup", type=int, default=200)
+ap.add_argument("--stream-priority", type=int, default=None,
+                help="run on a new torch stream of this priority (lower = higher priority)")
 a = ap.parse_args()
+if a.stream_priority is not None:
+    torch.cuda.set_stream(torch.cuda.Stream(priority=a.stream_priority))
 m = mb.SimManager(0, a.worlds, 69, 32)
 m.write_synthetic_actions(1234, 0)
 for t in range(a.warmup):
@@ -28,6 +32,7 @@ torch.cuda.synchronize()
 dt = time.perf_counter() - t0
 kt = m.kernel_times()
 out = {"lib": os.path.basename(os.environ.get("MBOTS_LIB", "default")),
+       "stream_priority": a.stream_priority,
        "agent_steps_per_s": (m.agent_steps() - s0) / dt, "ms_per_step": dt / a.steps * 1e3,
        "kernel_ms": {k: round(v[0] / v[1], 4) for k, v in kt.items() if v[1]}}
 print(json.dumps(out), flush=True)
