@@ -99,7 +99,8 @@ def secondary_run(W, args, rank, world_size, dev, distributed):
         m.step(); m.shift_observations(); m.write_synthetic_actions(ACTION_SEED, t + 1)
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
-    st = torch.tensor([el, float(m.agent_steps() - s0)], dtype=torch.float64, device=dev)
+    st = torch.tensor([el, float(m.agent_steps() - s0)], dtype=torch.float64,
+                      device=dev if args.backend == "nccl" else "cpu")
     if distributed:
         dist.barrier()
         tm = st[0:1].clone(); dist.all_reduce(tm, op=dist.ReduceOp.MAX)
@@ -125,6 +126,11 @@ def main():
     ap.add_argument("--no-kernel-timing", action="store_true")
     ap.add_argument("--gather", action="store_true",
                     help="config 5: construct_obs + RCCL gather of obs/reward rows to rank 0")
+    ap.add_argument("--backend", default="nccl",
+                    help="torch.distributed backend for the bench's barrier/max/sum (nccl = RCCL); "
+                         "gloo allows a rehearsal with several ranks on one GPU")
+    ap.add_argument("--same-device", action="store_true",
+                    help="rehearsal: every rank uses cuda:0 (with --backend gloo)")
     ap.add_argument("--no-secondary", action="store_true",
                     help="skip the 4096-worlds/GPU secondary measurement")
     args = ap.parse_args()
@@ -133,16 +139,18 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     distributed = world_size > 1
+    dev_index = 0 if (args.same_device or not distributed) else local_rank
+    torch.cuda.set_device(dev_index)
+    dev = torch.device("cuda", dev_index)
     if distributed:
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    else:
-        torch.cuda.set_device(0)
-    dev = torch.device("cuda", local_rank)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(args.backend)
 
     import madrona_bots as mb
     W = args.worlds
-    mgr = mb.SimManager(local_rank, W, SEED, AGENTS_PER_WORLD, world_offset=rank * W)
+    mgr = mb.SimManager(dev_index, W, SEED, AGENTS_PER_WORLD, world_offset=rank * W)
 
     gather_s = [0.0]
 
@@ -201,7 +209,8 @@ def main():
     secondary = None
     if not args.no_secondary and W != 4096:
         secondary = secondary_run(4096, args, rank, world_size, dev, distributed)
-    stats = torch.tensor([elapsed, float(agent_steps)], dtype=torch.float64, device=dev)
+    stats = torch.tensor([elapsed, float(agent_steps)], dtype=torch.float64,
+                         device=dev if args.backend == "nccl" else "cpu")
     if distributed:
         tmax = stats[0:1].clone()
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
