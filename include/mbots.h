@@ -125,6 +125,19 @@ int mbots_agent_offset_for_world(mbots_handle *h, uint32_t world, uint32_t *out)
 int mbots_construct_obs(mbots_handle *h, int32_t prev, float *out, uint64_t out_rows,
                         void *stream);
 
+/* Checkpoint / restore (the reference has none): the live state
+ * after the last step (agent SoA, RNG keys/counters, food, the current export
+ * table's N rows) as a host blob.  A manager created with the same
+ * configuration continues bit-exactly after mbots_load_checkpoint. */
+int mbots_checkpoint_size(mbots_handle *h, uint64_t *bytes);
+int mbots_save_checkpoint(mbots_handle *h, void *host_dst, uint64_t bytes);
+int mbots_load_checkpoint(mbots_handle *h, const void *host_src, uint64_t bytes);
+/* Debug dump of one world (viewer replacement): host arrays of agent_capacity
+ * rows -- (x, y, rot.w, rot.z) f32, (species, health, finder) i32 -- the 48
+ * packed food records, and the live agent count. */
+int mbots_world_state(mbots_handle *h, uint32_t world, float *xy_rwrz, int32_t *sp_hp_finder,
+                      uint64_t *food, int32_t *n_out);
+
 /* Build utilities (benchmark / test harness, not reference API):
  * identity-keyed synthetic action stream: one-hot(threefry(seed,step |
  * global_world, slot) % 6) written into the Action column of every live agent;

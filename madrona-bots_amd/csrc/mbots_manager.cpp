@@ -213,6 +213,51 @@ int record_totals(mbots_handle *h, hipStream_t st)
 
 }  // namespace
 
+// checkpoint segments (mbots_save_checkpoint / mbots_load_checkpoint)
+namespace {
+struct CkptHeader {
+    char magic[8];
+    uint32_t version, num_worlds, cap, A, world_offset, flags, seed, n_rows;
+    uint64_t bytes;
+};
+constexpr uint32_t kCkptVersion = 1;
+
+struct Seg {
+    void *p;
+    size_t bytes;
+};
+
+std::vector<Seg> ckpt_segments(mbots_handle *h, mbots::ObsTable &t, uint32_t n_rows)
+{
+    using namespace mbots;
+    SimState &S = h->S;
+    const size_t W = h->cfg.num_worlds, rows = W * h->cfg.agent_capacity, N = n_rows;
+    std::vector<Seg> v = {
+        {S.x, rows * 4}, {S.y, rows * 4}, {S.rw, rows * 4}, {S.rz, rows * 4},
+        {S.species, rows * 4}, {S.health, rows * 4}, {S.finder, rows * 4}, {S.obsrow, rows * 4},
+        {S.sur0, rows * 4}, {S.sur1, rows * 4}, {S.stats, rows * 4},
+        {S.n, W * 4}, {S.ctr, W * 4}, {S.key, W * 8}, {S.food, W * kNumChunks * 8},
+        {S.cur_food, W * 4}, {S.sreward, W * kNumSpecies * 4}, {S.scount, W * kNumSpecies * 4},
+        {S.row_base, W * kNumSpecies * 4}, {S.world_off, W * 4}, {S.overflow, W * 4},
+        {S.totals, 8 * 4}, {S.agent_steps, 8},
+        {t.species, N * 4}, {t.pos, N * 8}, {t.health, N * 4}, {t.sur, N * 8}, {t.reward, N * 4},
+        {t.action, N * 24}, {t.stats, N * 16}, {t.hidden, N * kHidden * 4},
+        {t.sem, N * kSensor}, {t.depth, N * kSensor},
+        {t.pspecies, N * 4}, {t.ppos, N * 8}, {t.phealth, N * 4}, {t.psur, N * 8},
+        {t.preward, N * 4}, {t.paction, N * 24}, {t.pstats, N * 16}, {t.phidden, N * kHidden * 4},
+        {t.psem, N * kSensor}, {t.pdepth, N * kSensor},
+    };
+    return v;
+}
+
+size_t ckpt_bytes(const std::vector<Seg> &v)
+{
+    size_t b = sizeof(CkptHeader);
+    for (const Seg &s : v) b += s.bytes;
+    return b;
+}
+}  // namespace
+
 extern "C" {
 
 const char *mbots_last_error(void) { return g_err.c_str(); }
@@ -513,6 +558,115 @@ int mbots_overflow(mbots_handle *h, uint64_t *out)
     uint64_t s = 0;
     for (uint32_t x : v) s += x;
     *out = s;
+    return MBOTS_OK;
+}
+
+// ---- checkpoint / restore (absent in the reference) ----
+// Blob: header + the live state after the last step: agent SoA columns (all
+// W x cap slots), per-world arrays, and the first N rows of every column of the
+// current export table.  Restoring into a manager of the same configuration
+// puts the table in half 0, clears the scan tiles and continues bit-exactly.
+int mbots_checkpoint_size(mbots_handle *h, uint64_t *out)
+{
+    if (!h || !out) return fail(MBOTS_E_INVALID, "null argument");
+    int rc = sync_totals(h);
+    if (rc) return rc;
+    *out = ckpt_bytes(ckpt_segments(h, h->T[h->tb], h->h_totals[0]));
+    return MBOTS_OK;
+}
+
+int mbots_save_checkpoint(mbots_handle *h, void *dst, uint64_t bytes)
+{
+    if (!h || !dst) return fail(MBOTS_E_INVALID, "null argument");
+    HIP_TRY(hipSetDevice(h->device));
+    HIP_TRY(hipDeviceSynchronize());   // the sensor's finder / semantic rows included
+    int rc = sync_totals(h);
+    if (rc) return rc;
+    const uint32_t n_rows = h->h_totals[0];
+    const auto segs = ckpt_segments(h, h->T[h->tb], n_rows);
+    const size_t need = ckpt_bytes(segs);
+    if (bytes < need) return fail(MBOTS_E_INVALID, "checkpoint buffer too small");
+    CkptHeader hd{};
+    memcpy(hd.magic, "MBOTSCK", 8);
+    hd.version = kCkptVersion;
+    hd.num_worlds = h->cfg.num_worlds;
+    hd.cap = h->cfg.agent_capacity;
+    hd.A = h->cfg.init_num_agents_per_world;
+    hd.world_offset = h->cfg.world_offset;
+    hd.flags = h->cfg.flags;
+    hd.seed = h->cfg.rand_seed;
+    hd.n_rows = n_rows;
+    hd.bytes = need;
+    char *p = static_cast<char *>(dst);
+    memcpy(p, &hd, sizeof(hd));
+    p += sizeof(hd);
+    for (const Seg &s : segs) {
+        if (s.bytes) HIP_TRY(hipMemcpy(p, s.p, s.bytes, hipMemcpyDeviceToHost));
+        p += s.bytes;
+    }
+    return MBOTS_OK;
+}
+
+int mbots_load_checkpoint(mbots_handle *h, const void *src, uint64_t bytes)
+{
+    if (!h || !src) return fail(MBOTS_E_INVALID, "null argument");
+    if (bytes < sizeof(CkptHeader)) return fail(MBOTS_E_INVALID, "checkpoint truncated");
+    CkptHeader hd;
+    memcpy(&hd, src, sizeof(hd));
+    if (memcmp(hd.magic, "MBOTSCK", 8) != 0 || hd.version != kCkptVersion)
+        return fail(MBOTS_E_INVALID, "not a checkpoint of this version");
+    if (hd.num_worlds != h->cfg.num_worlds || hd.cap != h->cfg.agent_capacity ||
+        hd.A != h->cfg.init_num_agents_per_world || hd.world_offset != h->cfg.world_offset ||
+        hd.flags != h->cfg.flags || hd.seed != h->cfg.rand_seed)
+        return fail(MBOTS_E_INVALID, "checkpoint configuration differs from the manager's");
+    if (hd.n_rows > (uint64_t)h->cfg.num_worlds * h->cfg.agent_capacity)
+        return fail(MBOTS_E_INVALID, "checkpoint row count out of range");
+    HIP_TRY(hipSetDevice(h->device));
+    HIP_TRY(hipDeviceSynchronize());
+    const auto segs = ckpt_segments(h, h->T[0], hd.n_rows);
+    if (bytes < ckpt_bytes(segs) || hd.bytes != ckpt_bytes(segs))
+        return fail(MBOTS_E_INVALID, "checkpoint size mismatch");
+    const char *p = static_cast<const char *>(src) + sizeof(hd);
+    for (const Seg &s : segs) {
+        if (s.bytes) HIP_TRY(hipMemcpy(s.p, p, s.bytes, hipMemcpyHostToDevice));
+        p += s.bytes;
+    }
+    HIP_TRY(hipMemset(h->S.tiles, 0, (size_t)2 * h->S.ntiles * 5 * sizeof(int32_t)));
+    h->tb = 0;
+    h->parity = 0;
+    h->last_join = -1;
+    h->steps = 1;
+    hipStream_t st = nullptr;
+    int rc = record_totals(h, st);
+    if (rc) return rc;
+    HIP_TRY(hipDeviceSynchronize());
+    return MBOTS_OK;
+}
+
+int mbots_world_state(mbots_handle *h, uint32_t world, float *xy_rwrz, int32_t *sp_hp_finder,
+                      uint64_t *food, int32_t *n_out)
+{
+    using namespace mbots;
+    if (!h || !xy_rwrz || !sp_hp_finder || !food || !n_out) return fail(MBOTS_E_INVALID, "null argument");
+    if (world >= h->cfg.num_worlds) return fail(MBOTS_E_INVALID, "world out of range");
+    HIP_TRY(hipSetDevice(h->device));
+    HIP_TRY(hipDeviceSynchronize());
+    const SimState &S = h->S;
+    const size_t cap = h->cfg.agent_capacity, base = (size_t)world * cap;
+    std::vector<float> f(cap);
+    std::vector<int32_t> v(cap);
+    const float *fc[4] = {S.x, S.y, S.rw, S.rz};
+    for (int c = 0; c < 4; ++c) {
+        HIP_TRY(hipMemcpy(f.data(), fc[c] + base, cap * 4, hipMemcpyDeviceToHost));
+        for (size_t i = 0; i < cap; ++i) xy_rwrz[i * 4 + c] = f[i];
+    }
+    const int32_t *ic[3] = {S.species, S.health, S.finder};
+    for (int c = 0; c < 3; ++c) {
+        HIP_TRY(hipMemcpy(v.data(), ic[c] + base, cap * 4, hipMemcpyDeviceToHost));
+        for (size_t i = 0; i < cap; ++i) sp_hp_finder[i * 3 + c] = v[i];
+    }
+    HIP_TRY(hipMemcpy(food, S.food + (size_t)world * kNumChunks, kNumChunks * 8, hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(n_out, S.n + world, 4, hipMemcpyDeviceToHost));
     return MBOTS_OK;
 }
 

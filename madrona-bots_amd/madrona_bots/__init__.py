@@ -56,6 +56,10 @@ def _load():
         "mbots_shift_observations": [vp, vp],
         "mbots_num_agents": [vp, P(u32)],
         "mbots_construct_obs": [vp, i32, vp, ctypes.c_uint64, vp],
+        "mbots_checkpoint_size": [vp, P(ctypes.c_uint64)],
+        "mbots_save_checkpoint": [vp, vp, ctypes.c_uint64],
+        "mbots_load_checkpoint": [vp, vp, ctypes.c_uint64],
+        "mbots_world_state": [vp, u32, vp, vp, vp, P(i32)],
         "mbots_export": [vp, i32, P(_CTensor)],
         "mbots_set_action": [vp, u32, P(i32)],
         "mbots_agent_offset_for_world": [vp, u32, P(u32)],
@@ -153,6 +157,7 @@ class SimManager:
                  fix_depth_alias=False):
         self.gpu_id = int(gpu_id)
         self.num_worlds = int(num_worlds)
+        self.agent_capacity = int(agent_capacity)
         flags = (FLAG_REWARD_FIXED if reward_fixed else 0) | \
                 (FLAG_FIX_DEPTH_ALIAS if fix_depth_alias else 0)
         cfg = _Config(self.gpu_id, self.num_worlds, int(rand_seed) & 0xFFFFFFFF,
@@ -256,6 +261,52 @@ class SimManager:
                                         ctypes.c_void_p(out.data_ptr()), out.shape[0],
                                         self._stream()))
         return out[:n]
+
+    def save_checkpoint(self, path=None):
+        """Live simulator state as bytes (and to `path` if given); see
+        load_checkpoint.  Not in the reference."""
+        import numpy as np
+        n = ctypes.c_uint64()
+        _check(_lib.mbots_checkpoint_size(self._h, ctypes.byref(n)))
+        buf = np.empty(n.value, dtype=np.uint8)
+        _check(_lib.mbots_save_checkpoint(self._h, ctypes.c_void_p(buf.ctypes.data), n.value))
+        if path is not None:
+            buf.tofile(path)
+        return buf
+
+    def load_checkpoint(self, src):
+        """Restore a checkpoint (bytes/array or a file path) saved by a manager
+        of the same configuration; the next step continues bit-exactly."""
+        import numpy as np
+        buf = np.fromfile(src, dtype=np.uint8) if isinstance(src, (str, os.PathLike)) \
+            else np.ascontiguousarray(np.frombuffer(src, dtype=np.uint8))
+        _check(_lib.mbots_load_checkpoint(self._h, ctypes.c_void_p(buf.ctypes.data), buf.size))
+
+    def world_state(self, world_idx):
+        """Debug dump of one world (replacing the viewer's
+        state readback): live agents' position, rotation (w, z), species,
+        health, finder slot, and the food packages (chunk, x, y) that are live,
+        as numpy arrays (save with numpy.savez)."""
+        import numpy as np
+        cap = self.agent_capacity
+        xyr = np.zeros((cap, 4), np.float32)
+        shf = np.zeros((cap, 3), np.int32)
+        food = np.zeros(48, np.uint64)
+        n = ctypes.c_int32()
+        _check(_lib.mbots_world_state(self._h, int(world_idx), ctypes.c_void_p(xyr.ctypes.data),
+                                      ctypes.c_void_p(shf.ctypes.data),
+                                      ctypes.c_void_p(food.ctypes.data), ctypes.byref(n)))
+        k = n.value
+        pk = []
+        for c, rec in enumerate(food.tolist()):
+            for q in range(5):
+                if (rec >> (40 + q)) & 1:
+                    xy = (rec >> (8 * q)) & 0xFF
+                    pk.append((c, (c % 8) * 16 + (xy & 15), (c // 8) * 16 + (xy >> 4)))
+        return {"position": xyr[:k, :2].copy(), "rotation_wz": xyr[:k, 2:].copy(),
+                "species": shf[:k, 0].copy(), "health": shf[:k, 1].copy(),
+                "finder": shf[:k, 2].copy(),
+                "food": np.array(pk, np.int32).reshape(-1, 3)}
 
     def write_synthetic_actions(self, seed, step, write_hidden=False):
         _check(_lib.mbots_write_synthetic_actions(self._h, int(seed) & 0xFFFFFFFF,
