@@ -7,9 +7,12 @@
 // species-major (species, world, slot) and written into the other half of a
 // double-buffered table every step.
 //
-// Step = K1 world_step (ECS systems + per-world compaction + per-tile species
-// counts) -> K2 scan (species-major row offsets) -> K3 export_sensor (row move,
-// observations, reward, raycast sensor) ; shift_observations = K5 shift.
+// step() = K1 world_step (ECS systems, per-world compaction into the other
+// state half, per-tile species counts) -> K2 scan (species-major row offsets)
+// -> fork: K3b sensor (raycast + finder, internal stream)  ||  K3a export_rows
+// (current observations, reward, old->new row map) -> K4 move (Action, Hidden,
+// Prev*, prev sensor to the new rows).  shift_observations() = K5 shift.
+// DESIGN.md section 4 has the schedule and each kernel's bound.
 #include "mbots_kernels.hpp"
 #include "mbots_ray.hpp"
 
