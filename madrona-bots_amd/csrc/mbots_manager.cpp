@@ -71,7 +71,7 @@ struct mbots_handle {
     int32_t *sensor_index = nullptr;  // scratch for sensorIndexTensor
     uint32_t *h_totals = nullptr;     // pinned mirror of S.totals
     hipEvent_t ev_totals = nullptr;
-    hipStream_t aux = nullptr;        // internal stream: K4 move next to the K3b sensor
+    hipStream_t aux = nullptr;        // internal stream of the K3b sensor (forked after K2)
     hipEvent_t ev_fork = nullptr;
     hipEvent_t ev_join[2] = {nullptr, nullptr};   // K3b of alternate steps done (aux)
     int last_join = -1;               // ev_join of the latest K3b, -1: none pending
