@@ -31,6 +31,9 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0       # MI355X HBM3E spec (MI355X_MICROARCH.md)
+# VALU issue peak: 256 CUs x 4 SIMDs, one wave64 VALU instruction per 2 cycles
+# per SIMD (32 lanes/cycle, MI355X_MICROARCH.md), 2.4 GHz
+VALU_PEAK_INSTR_S = 1024 * 2.4e9 / 2
 SEED = 69                   # learn/env.py:15
 ACTION_SEED = 1234
 AGENTS_PER_WORLD = 32       # learn/env.py:15
@@ -48,6 +51,20 @@ def load_traffic(worlds):
     import glob
     best = None
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_traffic.json"))):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        if d.get("worlds") == worlds:
+            best = (os.path.relpath(f, ROOT), d)
+    return best
+
+
+def load_profile(suffix, worlds):
+    """profiles/*_<suffix>.json recorded at `worlds` (the latest), or None."""
+    import glob
+    best = None
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", f"*_{suffix}.json"))):
         try:
             d = json.load(open(f))
         except (OSError, ValueError):
@@ -260,6 +277,18 @@ def main():
         if ktimes:
             per = {k: (ms / n if n else 0.0) for k, (ms, n) in ktimes.items()}
             out["kernel_ms"] = {k: round(v, 5) for k, v in per.items() if v}
+            vp = load_profile("valu", W)
+            sens = vp[1]["kernels"].get("sensor_kernel") if vp else None
+            if sens and per.get("sensor"):
+                rate = sens["SQ_INSTS_VALU"] / (per["sensor"] * 1e-3)
+                out["sensor_valu"] = {
+                    "bound": "valu-issue", "kernel": "K3b sensor (the step's critical path)",
+                    "valu_instr_per_launch": sens["SQ_INSTS_VALU"],
+                    "salu_instr_per_launch": sens.get("SQ_INSTS_SALU"),
+                    "launch_ms": per["sensor"], "achieved": rate, "peak": VALU_PEAK_INSTR_S,
+                    "unit": "wave64 VALU instr/s", "frac": rate / VALU_PEAK_INSTR_S,
+                    "source": vp[0],
+                    "note": "launch_ms is the sensor's event span inside the overlapped schedule"}
         if args.gather:
             out["config5"] = {"what": "step + fused construct_obs + RCCL gather of obs [N,69] f32 "
                                       "and reward rows to rank 0 (harness/gather.py) + shift",
