@@ -912,38 +912,38 @@ __global__ __launch_bounds__(64 * kSensorWorlds) void sensor_kernel(SimState S, 
         const int nc = min(kKeyAgents, n - a0);
         for (int q = lane; q < nc * kKeyStride; q += 64) L.key[q] = kNoKey;
         wave_sync();
-        // ---- P1: wedge pre-cull of the chunk's (agent, object) pairs ----
+        // ---- P1: wedge pre-cull of the chunk's (agent, object) pairs.  Lane =
+        // (agent a, object group o): the chunk's nc agents rounded up to P = 1,
+        // 2, 4 or 8 and G = 64 / P object groups, objects j = o + G t ----
         int nq = 0;
-        // flattened pair p = ic * nobj + j; advancing p by 64 = (q, r) with
-        // 64 = q * nobj + r (wave-uniform), then one conditional carry
-        const int adv_q = 64 / nobj, adv_r = 64 - adv_q * nobj;
-        int ic = (int)lane / nobj, j = (int)lane - ic * nobj;
-        const int npairs = nc * nobj;
-        for (int qb = 0; qb < npairs; qb += 64) {
-            bool keep = false;
-            if (ic < nc && j != nf + a0 + ic) {
-                float f, l;
-                uint32_t order;
-                pair_fl(L, nf, a0 + ic, j, f, l, order);
-                keep = fabsf(l) <= fabsf(f) + kWedge;
+        {
+            const int P = nc > 4 ? 8 : nc > 2 ? 4 : nc > 1 ? 2 : 1;
+            const int G = 64 / P, lgG = 6 - (P == 8 ? 3 : P == 4 ? 2 : P == 2 ? 1 : 0);
+            const int a = (int)lane >> lgG, o = (int)lane & (G - 1);
+            const int ia = a0 + min(a, nc - 1);
+            const float2 ap = L.obj[nf + ia], ah = L.hd[ia];
+            const int self = a < nc ? nf + ia : -1;
+            for (int jb = 0; jb < nobj; jb += G) {
+                const int j = jb + o;
+                bool keep = false;
+                if ((j < nobj) & (j != self) & (a < nc)) {
+                    const float2 p = L.obj[j];
+                    const float vx = p.x - ap.x, vy = p.y - ap.y;
+                    const float f = vx * ah.x + vy * ah.y, l = vx * ah.y - vy * ah.x;   // pair_fl
+                    keep = fabsf(l) <= fabsf(f) + kWedge;
+                }
+                const uint64_t m = ballot64(keep);
+                if (keep) L.qcode[nq + (int)rank_below(m)] = (uint32_t)a | ((uint32_t)j << 11);
+                nq += __popcll(m);
+                if (nq >= 64) {
+                    wave_sync();
+                    [[maybe_unused]] const unsigned long long ta = PROF_NOW();
+                    run_survivors(L, nf, a0, nq - 64, 64);
+                    PROF_ADD(2, PROF_NOW() - ta);
+                    PROF_ADD(5, 64);
+                    nq -= 64;
+                }
             }
-            const uint64_t m = ballot64(keep);
-            if (keep) L.qcode[nq + (int)rank_below(m)] = (uint32_t)ic | ((uint32_t)j << 11);
-            nq += __popcll(m);
-            if (nq >= 64) {
-                wave_sync();
-                [[maybe_unused]] const unsigned long long ta = PROF_NOW();
-                run_survivors(L, nf, a0, nq - 64, 64);
-                PROF_ADD(2, PROF_NOW() - ta);
-                PROF_ADD(5, 64);
-                nq -= 64;
-            }
-            // advance the flattened (agent, object) index by 64
-            j += adv_r;
-            ic += adv_q;
-            const bool carry = j >= nobj;
-            j -= carry ? nobj : 0;
-            ic += carry ? 1 : 0;
         }
         if (nq > 0) {
             wave_sync();
