@@ -518,6 +518,15 @@ __global__ __launch_bounds__(1024) void scan_kernel(SimState S, int parity)
         S.totals[0] = (uint32_t)s_tot[4];
         for (int k = 0; k < 4; ++k) S.totals[1 + k] = (uint32_t)s_tot[k];
         *S.agent_steps += (unsigned long long)s_tot[4];
+        // the host reads the row counts straight from pinned memory once the
+        // event after K2 completes (no D2H copy on the step's stream)
+        if (S.totals_host) {
+#pragma unroll
+            for (int k = 0; k < 5; ++k)
+                __hip_atomic_store(S.totals_host + k, k ? (uint32_t)s_tot[k - 1] : (uint32_t)s_tot[4],
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __threadfence_system();
+        }
     }
 }
 

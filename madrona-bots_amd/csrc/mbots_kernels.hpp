@@ -29,6 +29,7 @@ struct SimState {
     int32_t *src_of;                // [W*cap] new export row -> old row (-1: new agent)
     uint32_t *overflow;             // [W] dropped births/respawns
     uint32_t *totals;               // [0] = N, [1..4] = per-species rows
+    uint32_t *totals_host;          // mapped pinned mirror of totals (written by K2)
     int32_t *tiles;                 // [2][ntiles][5] per-tile species/agent counts (K1 -> K2)
     unsigned long long *agent_steps;
     // K1's output half of the double-buffered columns the sensor reads (the

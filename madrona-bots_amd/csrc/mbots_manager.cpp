@@ -72,7 +72,6 @@ struct mbots_handle {
     uint32_t *h_totals = nullptr;     // pinned mirror of S.totals
     hipEvent_t ev_totals = nullptr;
     hipStream_t aux = nullptr;        // internal stream of the K3b sensor (forked after K2)
-    hipEvent_t ev_fork = nullptr;
     hipEvent_t ev_join[2] = {nullptr, nullptr};   // K3b of alternate steps done (aux)
     int last_join = -1;               // ev_join of the latest K3b, -1: none pending
     uint64_t steps = 0;               // steps run
@@ -312,10 +311,12 @@ int mbots_create(const mbots_config *cfg_in, mbots_handle **out)
         if (e != hipSuccess && rc == MBOTS_OK)
             rc = fail(MBOTS_E_HIP, std::string(what) + ": " + hipGetErrorString(e));
     };
-    check(hipHostMalloc((void **)&h->h_totals, 8 * sizeof(uint32_t), hipHostMallocDefault),
+    check(hipHostMalloc((void **)&h->h_totals, 8 * sizeof(uint32_t), hipHostMallocMapped),
           "hipHostMalloc");
+    if (rc == MBOTS_OK)
+        check(hipHostGetDevicePointer((void **)&S.totals_host, h->h_totals, 0),
+              "hipHostGetDevicePointer");
     check(hipEventCreateWithFlags(&h->ev_totals, hipEventDisableTiming), "hipEventCreate");
-    check(hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming), "hipEventCreate");
     check(hipEventCreateWithFlags(&h->ev_join[0], hipEventDisableTiming), "hipEventCreate");
     check(hipEventCreateWithFlags(&h->ev_join[1], hipEventDisableTiming), "hipEventCreate");
     check(hipStreamCreateWithFlags(&h->aux, hipStreamNonBlocking), "hipStreamCreate");
@@ -350,7 +351,6 @@ int mbots_destroy(mbots_handle *h)
     for (auto &p : h->pending) { (void)hipEventDestroy(p.a); (void)hipEventDestroy(p.b); }
     for (auto e : h->pool) (void)hipEventDestroy(e);
     if (h->ev_totals) (void)hipEventDestroy(h->ev_totals);
-    if (h->ev_fork) (void)hipEventDestroy(h->ev_fork);
     for (auto e : h->ev_join) if (e) (void)hipEventDestroy(e);
     if (h->aux) (void)hipStreamDestroy(h->aux);
     if (h->h_totals) (void)hipHostFree(h->h_totals);
@@ -377,6 +377,8 @@ int mbots_step(mbots_handle *h, void *stream)
         return rc;
     mbots::swap_state(h->S);
     if ((rc = timed(h, MBOTS_TK_SCAN, st, [&] { return mbots::launch_scan(h->S, par, st); }))) return rc;
+    // K2 wrote the row counts into the pinned mirror; accessors wait on this
+    HIP_TRY(hipEventRecord(h->ev_totals, st));
 #ifdef MB_NO_FORK
     if ((rc = timed(h, MBOTS_TK_EXPORT, st,
                     [&] { return mbots::launch_export_rows(h->S, nxt, 0, st); })))
@@ -392,8 +394,7 @@ int mbots_step(mbots_handle *h, void *stream)
     // writes -- none of which reads the sensor rows or the finder slots.  The
     // next step's K1 and the semantic/depth accessors wait for ev_join.
     const int jcur = h->last_join == 0 ? 1 : 0;
-    HIP_TRY(hipEventRecord(h->ev_fork, st));
-    HIP_TRY(hipStreamWaitEvent(h->aux, h->ev_fork, 0));
+    HIP_TRY(hipStreamWaitEvent(h->aux, h->ev_totals, 0));
     if ((rc = timed(h, MBOTS_TK_SENSOR, h->aux, [&] { return mbots::launch_sensor(h->S, nxt, h->aux); })))
         return rc;
     HIP_TRY(hipEventRecord(h->ev_join[jcur], h->aux));
@@ -407,7 +408,7 @@ int mbots_step(mbots_handle *h, void *stream)
     ++h->steps;
     h->parity ^= 1;
     h->tb ^= 1;
-    return record_totals(h, st);
+    return MBOTS_OK;
 }
 
 int mbots_shift_observations(mbots_handle *h, void *stream)

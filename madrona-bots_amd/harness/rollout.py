@@ -41,9 +41,11 @@ def construct_obs(sim, start, end, prev=False):
                       sim.surrounding_tensor(prev).to_torch()[start:end, :]), dim=1)
 
 
-def random_rollout(sim, steps, seed=1234, shift_per_species=False, device=None):
+def random_rollout(sim, steps, seed=1234, shift_per_species=False, device=None, fused=False):
     """Random-action rollout (BASELINE config 2).  shift_per_species=True
-    reproduces the reference's shift inside the species loop."""
+    reproduces the reference's shift inside the species loop.
+    fused=True builds the observation rows with sim.construct_obs (one kernel
+    for all species, sliced per species) instead of the 5-way torch.cat."""
     gen = torch.Generator(device=device if device is not None else "cpu").manual_seed(seed)
     stats = {"steps": 0, "agent_steps": 0, "step_s": 0.0, "obs_rows": 0}
     for t in range(steps):
@@ -55,11 +57,18 @@ def random_rollout(sim, steps, seed=1234, shift_per_species=False, device=None):
         offsets = species_offsets(sim)
         action = sim.action_tensor(False).to_torch()
         new_actions = []
+        if fused:
+            obs_all = sim.construct_obs(False)
+            prev_all = sim.construct_obs(True) if t > 0 else None
         for sp, (s, e) in enumerate(offsets):
-            obs = construct_obs(sim, s, e, prev=False)
+            if fused and not (shift_per_species and sp > 0):
+                obs = obs_all[s:e]
+                prev = prev_all[s:e] if prev_all is not None else None
+            else:   # after a per-species shift the prev rows changed: rebuild
+                obs = construct_obs(sim, s, e, prev=False)
+                prev = construct_obs(sim, s, e, prev=True) if t > 0 else None
             assert obs.shape == (e - s, OBS_DIM) and obs.dtype == torch.float32
-            if t > 0:
-                prev = construct_obs(sim, s, e, prev=True)
+            if prev is not None:
                 assert prev.shape == obs.shape
             stats["obs_rows"] += e - s
             a = torch.randint(0, ACTION_DIM, (e - s,), generator=gen, device=gen.device)
@@ -84,13 +93,14 @@ def main():
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--seed", type=int, default=69)
     ap.add_argument("--agents", type=int, default=32)
+    ap.add_argument("--fused", action="store_true", help="sim.construct_obs instead of torch.cat")
     a = ap.parse_args()
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     import madrona_bots as mb
     dev = torch.device("cuda", 0)
     sim = mb.SimManager(0, a.worlds, a.seed, a.agents)
-    random_rollout(sim, 5, device=dev)
-    st = random_rollout(sim, a.steps, device=dev)
+    random_rollout(sim, 5, device=dev, fused=a.fused)
+    st = random_rollout(sim, a.steps, device=dev, fused=a.fused)
     # the reference's "Average FPS for simulator" = num_worlds / mean step time
     print(json.dumps({"worlds": a.worlds, "steps": st["steps"],
                       "world_steps_per_s": a.worlds * st["steps"] / st["step_s"],

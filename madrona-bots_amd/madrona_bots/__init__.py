@@ -308,6 +308,18 @@ class SimManager:
                 "finder": shf[:k, 2].copy(),
                 "food": np.array(pk, np.int32).reshape(-1, 3)}
 
+    def dump_worlds(self, path, worlds):
+        """Write world_state() of each world in `worlds` to one .npz
+        (keys "w<idx>/<field>") for offline inspection -- the build's
+        replacement for the reference viewer's readback (src/gfx)."""
+        import numpy as np
+        arrays = {}
+        for w in worlds:
+            for k, v in self.world_state(w).items():
+                arrays[f"w{int(w)}/{k}"] = v
+        np.savez(path, **arrays)
+        return sorted(arrays)
+
     def write_synthetic_actions(self, seed, step, write_hidden=False):
         _check(_lib.mbots_write_synthetic_actions(self._h, int(seed) & 0xFFFFFFFF,
                                                   int(step) & 0xFFFFFFFF,
