@@ -698,7 +698,7 @@ __global__ __launch_bounds__(256) void move_kernel(const uint32_t *totals, const
 #define MB_KEY_AGENTS 8
 #endif
 #ifndef MB_ABL
-#define MB_ABL 0                              // timing ablations: 1 no sensor work, 8 no output
+#define MB_ABL 0   // timing ablations: 1 no sensor work, 8 no output, 16 no survivors, 32 no pixel tests, 64 no wide pairs
 #endif
 constexpr int kKeyAgents = MB_KEY_AGENTS;     // agents per chunk (key rows)
 constexpr int kKeyStride = 36;                // key row: 32 pixels, finder, pad (16-B rows)
@@ -745,7 +745,7 @@ __device__ __forceinline__ void pair_fl(const SensorLDS &L, int nf, int i, int j
 // each half also takes the finder ray)
 __device__ __forceinline__ void run_wide(SensorLDS &L, int nf, int cnt)
 {
-    if (MB_ABL & 32) return;
+    if (MB_ABL & (32 | 64)) return;
     const int lane = (int)__lane_id();
     for (int e0 = 0; e0 < cnt; e0 += 2) {
         const int e = e0 + (lane >> 5);
@@ -766,7 +766,8 @@ __device__ __forceinline__ void run_wide(SensorLDS &L, int nf, int cnt)
 
 // P2: survivors [q0, q0 + cnt): approximate roots bound the candidate pixels;
 // <= 2 pixels + the finder are tested inline, wider pairs go to the wide list
-__device__ __forceinline__ void run_survivors(SensorLDS &L, int nf, int a0, int q0, int cnt)
+__device__ __forceinline__ void run_survivors(SensorLDS &L, int nf, int a0, int q0, int cnt,
+                                              unsigned long long &nwide)
 {
     if (MB_ABL & 16) return;
     const int lane = (int)__lane_id();
@@ -793,17 +794,23 @@ __device__ __forceinline__ void run_survivors(SensorLDS &L, int nf, int a0, int 
             const int k1 = min((int)floorf(hi), (int)kmax);
             const int c = k1 - k0 + 1;
             k0 += fwd ? 0 : 24;
-            if (c > 2) {
-                wide = true;
-            } else if (!(MB_ABL & 32)) {
+            if (!(MB_ABL & 32)) {
+                // the two edge pixels of [k0, k0 + c) get the exact predicate;
+                // interior pixels lie >= one pixel pitch minus kUEps (>= 0.08 in
+                // u) inside the root interval of a pair with r > 1, |f| > 1.5,
+                // where the approximate roots are off by ~1e-6 and the float
+                // q(u) by < 1e-4: they are hits carrying the object's key
                 uint32_t *kr = L.key + ic * kKeyStride;
-                const float ua = L.u[k0 & 31], ub = L.u[(k0 + 1) & 31];
+                const int kl = k0 + max(c - 1, 0);
+                const float ua = L.u[k0 & 31], ub = L.u[kl & 31];
                 const uint32_t ka = pixel_key(f, l, ua, fwd, order);
                 const uint32_t kb = pixel_key(f, l, ub, fwd, order);
                 const uint32_t kf = finder_key(f, l, order);
                 if ((c > 0) & (ka != kNoKey)) atomicMin(&kr[k0], ka);
-                if ((c > 1) & (kb != kNoKey)) atomicMin(&kr[k0 + 1], kb);
+                if ((c > 1) & (kb != kNoKey)) atomicMin(&kr[kl], kb);
                 if (fwd & (u1 <= 0.0f) & (u2 >= 0.0f) & (kf != kNoKey)) atomicMin(&kr[kSensor], kf);
+                const uint32_t kin = zkey(max0(fwd ? f - 1.0f : -f - 1.0f), order);
+                for (int k = k0 + 1; k < kl; ++k) atomicMin(&kr[k], kin);
             }
         }
     }
@@ -815,6 +822,7 @@ __device__ __forceinline__ void run_survivors(SensorLDS &L, int nf, int a0, int 
         L.wl[s] = l;
     }
     const int nw = __popcll(wm);
+    nwide += (unsigned long long)nw;
     if (nw > 0) {
         wave_sync();
         run_wide(L, nf, nw);
@@ -865,6 +873,7 @@ __global__ __launch_bounds__(64 * kSensorWorlds) void sensor_kernel(SimState S, 
     if (lane < kSensor) L.u[lane] = kURay[lane];
     SensorPrefetch pf;
     sensor_prefetch(S, w, lane, pf);
+    [[maybe_unused]] unsigned long long wide_n = 0;
     do {
     [[maybe_unused]] const unsigned long long t_start = PROF_NOW();
     const size_t base = (size_t)w * S.cap;
@@ -947,7 +956,7 @@ __global__ __launch_bounds__(64 * kSensorWorlds) void sensor_kernel(SimState S, 
                 if (nq >= 64) {
                     wave_sync();
                     [[maybe_unused]] const unsigned long long ta = PROF_NOW();
-                    run_survivors(L, nf, a0, nq - 64, 64);
+                    run_survivors(L, nf, a0, nq - 64, 64, wide_n);
                     PROF_ADD(2, PROF_NOW() - ta);
                     PROF_ADD(5, 64);
                     nq -= 64;
@@ -957,7 +966,7 @@ __global__ __launch_bounds__(64 * kSensorWorlds) void sensor_kernel(SimState S, 
         if (nq > 0) {
             wave_sync();
             [[maybe_unused]] const unsigned long long ta = PROF_NOW();
-            run_survivors(L, nf, a0, 0, nq);
+            run_survivors(L, nf, a0, 0, nq, wide_n);
             PROF_ADD(2, PROF_NOW() - ta);
             PROF_ADD(5, nq);
         }
@@ -1010,6 +1019,7 @@ __global__ __launch_bounds__(64 * kSensorWorlds) void sensor_kernel(SimState S, 
         PROF_ADD(3, PROF_NOW() - to);
     }
 #ifdef MB_PROF
+    prof[1] += wide_n;
     prof[4] += PROF_NOW() - t_start;
     prof[6] += (unsigned long long)n * (unsigned long long)(nf + n);
     prof[7] += 1;

@@ -169,7 +169,7 @@ class SimManager:
 
     def __del__(self):
         h = getattr(self, "_h", None)
-        if h:
+        if h and _lib is not None:   # module globals may be gone at interpreter exit
             _lib.mbots_destroy(h)
             self._h = None
 

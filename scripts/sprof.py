@@ -31,6 +31,7 @@ v = list(buf)
 nw = v[7]
 names = ["staging", "p1_excl", "survivors", "output", "total", "n_survivors", "pairs"]
 out = {k: v[i] / nw for i, k in enumerate(names) if i not in (1,)}
+out["n_wide"] = v[1] / nw
 out["p1_excl"] = (v[4] - v[0] - v[2] - v[3]) / nw
 k = v[8:]
 kn = k[7] or 1
