@@ -164,7 +164,33 @@ __device__ void world_step(SimState &S, const ObsTable &cur, WorldLDS &L, uint32
     // row_hi): only the slot's own lane reads them (action fetch, compaction).
     int2 pa0 = make_int2(0, 0), pa1 = pa0, pa2 = pa0;
     int32_t row_lo = -1, row_hi = -1;
-    for (int i = lane; i < n0; i += 64) {
+    {
+        // slots < 64: loaded without waiting for n0 (slots past n0 are stale
+        // and dropped), so only the action rows wait on a second round trip
+        const bool in = lane < cap;
+        const size_t i = base + lane;
+        const int32_t row = in ? S.obsrow[i] : -1;
+        const float x = in ? S.x[i] : 0.0f, y = in ? S.y[i] : 0.0f;
+        const float rw = in ? S.rw[i] : 0.0f, rz = in ? S.rz[i] : 0.0f;
+        const int32_t sp = in ? S.species[i] : 0, hp = in ? S.health[i] : 0;
+        const int32_t fd = in ? S.finder[i] : -1;
+        if ((int)lane < n0) {
+            row_lo = row;
+            if (row >= 0) {
+                const int2 *ap = reinterpret_cast<const int2 *>(cur.action + (size_t)row * 6);
+                pa0 = ap[0]; pa1 = ap[1]; pa2 = ap[2];
+            }
+            L.x[lane] = x;
+            L.y[lane] = y;
+            L.rw[lane] = rw;
+            L.rz[lane] = rz;
+            L.species[lane] = (int8_t)sp;
+            L.accum[lane] = hp;
+            L.finder[lane] = (int8_t)fd;
+            L.flags[lane] = (uint8_t)F_ALIVE;
+        }
+    }
+    for (int i = 64 + lane; i < n0; i += 64) {
         const int32_t row = S.obsrow[base + i];
         if (i < 64) row_lo = row;
         else row_hi = row;
@@ -833,7 +859,7 @@ __device__ __forceinline__ void run_survivors(SensorLDS &L, int nf, int a0, int 
 // the world's staged inputs, loaded as one batch of independent loads
 struct SensorPrefetch {
     uint64_t food;             // lane < 48: packed chunk record
-    float x, y, rw, rz;        // lane < min(cap, 64): agent slot `lane`
+    float x, y, rw, rz;        // lane < min(n, 64): agent slot `lane`
     int32_t sp;
     int n;
 };
@@ -843,7 +869,7 @@ __device__ __forceinline__ void sensor_prefetch(const SimState &S, uint32_t w, u
 {
     p.n = uniform(S.n[w]);
     p.food = lane < kNumChunks ? S.food[(size_t)w * kNumChunks + lane] : 0ull;
-    if (lane < S.cap) {   // rows past n are allocated (stale); only [0, n) is staged
+    if ((int)lane < p.n) {   // slots [0, n) (rows past n are stale)
         const size_t i = (size_t)w * S.cap + lane;
         p.x = S.x[i];
         p.y = S.y[i];

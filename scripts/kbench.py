@@ -15,6 +15,7 @@ ap.add_argument("--steps", type=int, default=40)
 ap.add_argument("--warmup", type=int, default=200)
 ap.add_argument("--stream-priority", type=int, default=None,
                 help="run on a new torch stream of this priority (lower = higher priority)")
+ap.add_argument("--no-kernel-timing", action="store_true")
 a = ap.parse_args()
 if a.stream_priority is not None:
     torch.cuda.set_stream(torch.cuda.Stream(priority=a.stream_priority))
@@ -23,7 +24,7 @@ m.write_synthetic_actions(1234, 0)
 for t in range(a.warmup):
     m.step(); m.shift_observations(); m.write_synthetic_actions(1234, t + 1)
 torch.cuda.synchronize()
-m.enable_kernel_timing(True)
+m.enable_kernel_timing(not a.no_kernel_timing)
 s0 = m.agent_steps()
 t0 = time.perf_counter()
 for t in range(a.warmup, a.warmup + a.steps):
