@@ -14,6 +14,7 @@
 // Prev*, prev sensor to the new rows).  shift_observations() = K5 shift.
 // DESIGN.md section 4 has the schedule and each kernel's bound.
 #include "mbots_kernels.hpp"
+#include <stdlib.h>
 #include "mbots_ray.hpp"
 
 namespace mbots {
@@ -28,6 +29,33 @@ __device__ unsigned long long g_kprof[64 * 8];
 #else
 #define PROF_NOW() 0ull
 #define PROF_ADD(k, v) ((void)0)
+#endif
+
+#ifdef MB_TL
+// kernel timeline (instrumentation builds only): per launch of each kernel the
+// earliest wave start and latest wave end on the 100 MHz realtime clock, so a
+// step's schedule (gaps, overlap) is seen without a profiler in the process.
+// launch index = wave ticket / waves per launch (launches of one kernel never
+// overlap: each kernel has a single stream).
+constexpr int kTlKernels = 8, kTlSlots = 64, kTlSpread = 64;
+// [slot][kernel][spread][start, end]; spread = blockIdx & 63 keeps the
+// recording atomics off one address
+__device__ unsigned long long g_tl[kTlSlots * kTlKernels * kTlSpread * 2];
+struct TLScope {
+    unsigned long long *rec;
+    __device__ TLScope(int k, uint32_t step)
+        : rec(&g_tl[(((step % kTlSlots) * kTlKernels + k) * kTlSpread + (blockIdx.x & 63u)) * 2])
+    {
+        if (threadIdx.x == 0) atomicMin(&rec[0], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+    }
+    __device__ ~TLScope()
+    {
+        if (__lane_id() == 0) atomicMax(&rec[1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+    }
+};
+#define TL_SCOPE(k, step) TLScope tl_scope_(k, step)
+#else
+#define TL_SCOPE(k, step) ((void)0)
 #endif
 
 constexpr int kWorldsPerBlock = 4;
@@ -124,6 +152,7 @@ __device__ void world_step(SimState &S, const ObsTable &cur, WorldLDS &L, uint32
 
 __global__ __launch_bounds__(256, 8) void world_step_kernel(SimState S, ObsTable cur, int parity)
 {
+    TL_SCOPE(0, S.tl_step);
     __shared__ WorldLDS lds[kWorldsPerBlock];
     __shared__ int32_t blk[kWorldsPerBlock][5];
     const uint32_t wv = threadIdx.x >> 6;
@@ -492,6 +521,7 @@ __device__ __forceinline__ int wave_incl_scan(int v)
 
 __global__ __launch_bounds__(1024) void scan_kernel(SimState S, int parity)
 {
+    TL_SCOPE(1, S.tl_step);
     __shared__ int32_t s_pre[5], s_tot[5];
     __shared__ int32_t s_wave[16][5];
     const int t = threadIdx.x, b = blockIdx.x;
@@ -593,6 +623,7 @@ __global__ __launch_bounds__(1024) void tile_sum_kernel(SimState S, int parity)
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void export_rows_kernel(SimState S, ObsTable nxt, int init)
 {
+    TL_SCOPE(2, S.tl_step);
     const uint32_t wv = threadIdx.x >> 6;
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t w = uniform(blockIdx.x * kWorldsPerBlock + wv);
@@ -678,8 +709,9 @@ __device__ __forceinline__ void move_item(const MoveSeg &sg, uint32_t idx, int32
 }
 
 __global__ __launch_bounds__(256) void move_kernel(const uint32_t *totals, const int32_t *src_of,
-                                                   MoveArgs args)
+                                                   MoveArgs args, uint32_t tl_step)
 {
+    TL_SCOPE(4, tl_step);
     const uint32_t N = totals[0];
     const MoveSeg &sg = args.seg[blockIdx.y];
     const uint32_t items = N * sg.ipr;
@@ -886,6 +918,7 @@ __device__ __forceinline__ void sensor_prefetch(const SimState &S, uint32_t w, u
 constexpr int kSensorWorlds = MB_SENSOR_WPB;   // worlds (waves) per sensor block
 __global__ __launch_bounds__(64 * kSensorWorlds) void sensor_kernel(SimState S, ObsTable nxt)
 {
+    TL_SCOPE(3, S.tl_step);
     __shared__ SensorLDS lds[kSensorWorlds];
     const uint32_t wv = threadIdx.x >> 6;
     const uint32_t lane = threadIdx.x & 63u;
@@ -1060,6 +1093,30 @@ __global__ __launch_bounds__(64 * kSensorWorlds) void sensor_kernel(SimState S, 
 #endif
 }
 
+#ifdef MB_TL
+// timeline dump: out[slot][kernel][start, end] (realtime ticks; min / max over
+// the spread); clears the record
+extern "C" __attribute__((visibility("default"))) int mbots_debug_timeline(unsigned long long *out)
+{
+    static unsigned long long buf[kTlSlots * kTlKernels * kTlSpread * 2];
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(buf, HIP_SYMBOL(g_tl), sizeof(buf)) != hipSuccess) return -1;
+    for (int i = 0; i < kTlSlots * kTlKernels; ++i) {
+        unsigned long long lo = ~0ull, hi = 0ull;
+        for (int j = 0; j < kTlSpread; ++j) {
+            const unsigned long long a = buf[(i * kTlSpread + j) * 2], b = buf[(i * kTlSpread + j) * 2 + 1];
+            if (a && a < lo) lo = a;
+            if (b > hi) hi = b;
+        }
+        out[2 * i] = lo;
+        out[2 * i + 1] = hi;
+    }
+    for (int i = 0; i < kTlSlots * kTlKernels * kTlSpread; ++i) { buf[2 * i] = ~0ull; buf[2 * i + 1] = 0ull; }
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_tl), buf, sizeof(buf)) != hipSuccess) return -1;
+    return 0;
+}
+#endif
+
 #ifdef MB_PROF
 extern "C" __attribute__((visibility("default"))) int mbots_debug_sensor_prof(unsigned long long *out)
 {
@@ -1118,8 +1175,9 @@ __global__ __launch_bounds__(256) void construct_obs_kernel(const uint32_t *tota
 // 256-B allocation padding / unused capacity rows).  PrevStats rows get the
 // reference's prevStats.hitEnemyAgent = stats.hitFriendlyAgent (sim.cpp:1034).
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void shift_kernel(const uint32_t *totals, ObsTable t)
+__global__ __launch_bounds__(256) void shift_kernel(const uint32_t *totals, ObsTable t, uint32_t tl_step)
 {
+    TL_SCOPE(5, tl_step);
     const uint32_t N = totals[0];
     const uint32_t g4 = (4u * N + 15u) >> 4, g8 = (8u * N + 15u) >> 4, g24 = (24u * N + 15u) >> 4;
     // segment ends (in granules): species, pos, health, sur, reward, action, stats, hidden
@@ -1194,6 +1252,7 @@ __global__ __launch_bounds__(256) void synthetic_actions_kernel(SimState S, ObsT
                                                                 uint32_t seed, uint32_t step,
                                                                 int write_hidden)
 {
+    TL_SCOPE(6, S.tl_step);
     const uint32_t wv = threadIdx.x >> 6;
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t w = uniform(blockIdx.x * kWorldsPerBlock + wv);
@@ -1282,18 +1341,23 @@ hipError_t launch_move(const SimState &S, const ObsTable &cur, const ObsTable &n
     add(nxt.psem, cur.sem, 16, 2);                   // prev sensor <- last step's sensor
     if (S.flags & kFlagFixDepth) add(nxt.pdepth, cur.depth, 16, 2);
     m.nseg = k;
-    hipLaunchKernelGGL(move_kernel, dim3(512, k), dim3(256), 0, st, S.totals, S.src_of, m);
+    hipLaunchKernelGGL(move_kernel, dim3(512, k), dim3(256), 0, st, S.totals, S.src_of, m, S.tl_step);
     return hipGetLastError();
 }
 hipError_t launch_sensor(const SimState &S, const ObsTable &nxt, hipStream_t st)
 {
+    size_t pad = 0;
+#ifdef MB_KNOBS
+    // occupancy experiment: extra dynamic LDS per sensor block
+    if (const char *e = getenv("MBOTS_SENSOR_LDS_PAD")) pad = (size_t)atol(e);
+#endif
     hipLaunchKernelGGL(sensor_kernel, dim3((S.W + kSensorWorlds - 1) / kSensorWorlds),
-                       dim3(64 * kSensorWorlds), 0, st, S, nxt);
+                       dim3(64 * kSensorWorlds), pad, st, S, nxt);
     return hipGetLastError();
 }
 hipError_t launch_shift(const SimState &S, const ObsTable &t, hipStream_t st)
 {
-    hipLaunchKernelGGL(shift_kernel, dim3(4096), dim3(256), 0, st, S.totals, t);
+    hipLaunchKernelGGL(shift_kernel, dim3(4096), dim3(256), 0, st, S.totals, t, S.tl_step);
     return hipGetLastError();
 }
 hipError_t launch_synthetic_actions(const SimState &S, const ObsTable &t, uint32_t seed,

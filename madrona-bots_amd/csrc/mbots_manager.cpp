@@ -11,6 +11,7 @@
 //    rows (288 GB HBM per GPU leaves ample headroom);
 //  * the species-major export table is double-buffered: a step writes the new
 //    table while reading the old one (no in-place radix sort of 264-B rows).
+#include <hip/hip_ext.h>
 #include "../../include/mbots.h"
 #include "mbots_kernels.hpp"
 
@@ -319,6 +320,19 @@ int mbots_create(const mbots_config *cfg_in, mbots_handle **out)
     check(hipEventCreateWithFlags(&h->ev_totals, hipEventDisableTiming), "hipEventCreate");
     check(hipEventCreateWithFlags(&h->ev_join[0], hipEventDisableTiming), "hipEventCreate");
     check(hipEventCreateWithFlags(&h->ev_join[1], hipEventDisableTiming), "hipEventCreate");
+#ifdef MB_KNOBS
+    // occupancy experiment: the sensor stream on a CU subset spread evenly
+    if (const char *e = getenv("MBOTS_SENSOR_CUS")) {
+        hipDeviceProp_t prop;
+        check(hipGetDeviceProperties(&prop, cfg.gpu_id), "hipGetDeviceProperties");
+        const int ncu = prop.multiProcessorCount, k = atoi(e);
+        std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
+        for (int i = 0; i < ncu; ++i)
+            if ((i + 1) * k / ncu > i * k / ncu) mask[i / 32] |= 1u << (i % 32);
+        check(hipExtStreamCreateWithCUMask(&h->aux, (uint32_t)mask.size(), mask.data()),
+              "hipExtStreamCreateWithCUMask");
+    } else
+#endif
     check(hipStreamCreateWithFlags(&h->aux, hipStreamNonBlocking), "hipStreamCreate");
     hipStream_t st = nullptr;
     check(hipMemsetAsync(h->arena.base, 0, bytes, st), "hipMemsetAsync");
@@ -365,6 +379,7 @@ int mbots_step(mbots_handle *h, void *stream)
     HIP_TRY(hipSetDevice(h->device));
     hipStream_t st = as_stream(stream);
     h->last_stream = st;
+    h->S.tl_step = (uint32_t)h->steps;
     const mbots::ObsTable &cur = h->T[h->tb];
     const mbots::ObsTable &nxt = h->T[h->tb ^ 1];
     int rc;
