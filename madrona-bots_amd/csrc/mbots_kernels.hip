@@ -693,6 +693,8 @@ struct MoveSeg {
     const void *src;
     uint32_t width;   // bytes per item: 4, 8 or 16
     uint32_t ipr;     // items per row
+    uint32_t xform;   // 1: the source is current AgentStats, apply the shift's
+                      // prevStats.hitEnemy = stats.hitFriendly (sim.cpp:1034)
 };
 constexpr int kMaxMoveSegs = 13;
 struct MoveArgs {
@@ -722,7 +724,12 @@ __global__ __launch_bounds__(256) void move_kernel(const uint32_t *totals, const
         else if (sg.ipr == 3) { r = idx / 3u; part = idx - r * 3u; }
         else if (sg.ipr == 4) { r = idx >> 2; part = idx & 3u; }
         const int32_t o = src_of[r];
-        if (sg.width == 16) move_item<uint4>(sg, idx, o, part);
+        if (sg.width == 16 && sg.xform) {
+            uint4 v = make_uint4(0u, 0u, 0u, 0u);
+            if (o >= 0) v = reinterpret_cast<const uint4 *>(sg.src)[o];
+            v.y = v.x;
+            reinterpret_cast<uint4 *>(sg.dst)[idx] = v;
+        } else if (sg.width == 16) move_item<uint4>(sg, idx, o, part);
         else if (sg.width == 8) move_item<uint2>(sg, idx, o, part);
         else move_item<uint32_t>(sg, idx, o, part);
     }
@@ -1171,18 +1178,30 @@ __global__ __launch_bounds__(256) void construct_obs_kernel(const uint32_t *tota
 // K5: shiftObservationsSystem + shiftHiddenState (sim.cpp:1002-1048): Prev* <-
 // current for rows [0, N).  Each column is a contiguous byte range, so the copy
 // is one grid-stride stream of 16-byte granules over the concatenation of the
-// 8 columns (N is read on the device; granules past a column's end land in its
+// columns (N is read on the device; granules past a column's end land in its
 // 256-B allocation padding / unused capacity rows).  PrevStats rows get the
 // reference's prevStats.hitEnemyAgent = stats.hitFriendlyAgent (sim.cpp:1034).
+//
+// Lazy shift: between shift_observations() and the next step() only the
+// learner writes the table, and only its Action / HiddenState columns
+// (training_loop.py:136-137).  So the shift copies those two eagerly
+// (kShiftEager) and leaves Prev{Species, Position, Health, Surrounding,
+// Reward, Stats} as a view of the current columns: the next step moves them
+// from there, construct_obs reads them there, and an accessor of one of them
+// materialises the copy first (kShiftRest).  kShiftAll copies all eight.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void shift_kernel(const uint32_t *totals, ObsTable t, uint32_t tl_step)
+__global__ __launch_bounds__(256) void shift_kernel(const uint32_t *totals, ObsTable t, int mode,
+                                                    uint32_t tl_step)
 {
     TL_SCOPE(5, tl_step);
     const uint32_t N = totals[0];
-    const uint32_t g4 = (4u * N + 15u) >> 4, g8 = (8u * N + 15u) >> 4, g24 = (24u * N + 15u) >> 4;
+    const bool eager = mode != kShiftRest, rest = mode != kShiftEager;
+    const uint32_t g4 = rest ? (4u * N + 15u) >> 4 : 0u, g8 = rest ? (8u * N + 15u) >> 4 : 0u;
+    const uint32_t g24 = eager ? (24u * N + 15u) >> 4 : 0u;
+    const uint32_t gst = rest ? N : 0u, ghd = eager ? 4u * N : 0u;
     // segment ends (in granules): species, pos, health, sur, reward, action, stats, hidden
     const uint32_t e0 = g4, e1 = e0 + g8, e2 = e1 + g4, e3 = e2 + g8, e4 = e3 + g4,
-                   e5 = e4 + g24, e6 = e5 + N, e7 = e6 + 4u * N;
+                   e5 = e4 + g24, e6 = e5 + gst, e7 = e6 + ghd;
     const uint32_t stride = gridDim.x * blockDim.x;
     for (uint32_t g = blockIdx.x * blockDim.x + threadIdx.x; g < e7; g += stride) {
         const uint4 *src;
@@ -1321,22 +1340,25 @@ hipError_t launch_export_rows(const SimState &S, const ObsTable &nxt, int init, 
     hipLaunchKernelGGL(export_rows_kernel, dim3(world_blocks(S.W)), dim3(256), 0, st, S, nxt, init);
     return hipGetLastError();
 }
-hipError_t launch_move(const SimState &S, const ObsTable &cur, const ObsTable &nxt, hipStream_t st)
+hipError_t launch_move(const SimState &S, const ObsTable &cur, const ObsTable &nxt, int prev_lazy,
+                       hipStream_t st)
 {
     MoveArgs m{};
     int k = 0;
-    auto add = [&](void *d, const void *s, uint32_t width, uint32_t ipr) {
-        m.seg[k++] = MoveSeg{d, s, width, ipr};
+    auto add = [&](void *d, const void *s, uint32_t width, uint32_t ipr, uint32_t xform = 0) {
+        m.seg[k++] = MoveSeg{d, s, width, ipr, xform};
     };
+    // after a lazy shift the six Prev* columns it left are the current ones
+    const bool lz = prev_lazy != 0;
     add(nxt.action, cur.action, 8, 3);
     add(nxt.hidden, cur.hidden, 16, 4);
-    add(nxt.pspecies, cur.pspecies, 4, 1);
-    add(nxt.ppos, cur.ppos, 8, 1);
-    add(nxt.phealth, cur.phealth, 4, 1);
-    add(nxt.psur, cur.psur, 8, 1);
-    add(nxt.preward, cur.preward, 4, 1);
+    add(nxt.pspecies, lz ? cur.species : cur.pspecies, 4, 1);
+    add(nxt.ppos, lz ? cur.pos : cur.ppos, 8, 1);
+    add(nxt.phealth, lz ? cur.health : cur.phealth, 4, 1);
+    add(nxt.psur, lz ? cur.sur : cur.psur, 8, 1);
+    add(nxt.preward, lz ? cur.reward : cur.preward, 4, 1);
     add(nxt.paction, cur.paction, 8, 3);
-    add(nxt.pstats, cur.pstats, 16, 1);
+    add(nxt.pstats, lz ? cur.stats : cur.pstats, 16, 1, lz ? 1u : 0u);
     add(nxt.phidden, cur.phidden, 16, 4);
     add(nxt.psem, cur.sem, 16, 2);                   // prev sensor <- last step's sensor
     if (S.flags & kFlagFixDepth) add(nxt.pdepth, cur.depth, 16, 2);
@@ -1355,9 +1377,9 @@ hipError_t launch_sensor(const SimState &S, const ObsTable &nxt, hipStream_t st)
                        dim3(64 * kSensorWorlds), pad, st, S, nxt);
     return hipGetLastError();
 }
-hipError_t launch_shift(const SimState &S, const ObsTable &t, hipStream_t st)
+hipError_t launch_shift(const SimState &S, const ObsTable &t, int mode, hipStream_t st)
 {
-    hipLaunchKernelGGL(shift_kernel, dim3(4096), dim3(256), 0, st, S.totals, t, S.tl_step);
+    hipLaunchKernelGGL(shift_kernel, dim3(4096), dim3(256), 0, st, S.totals, t, mode, S.tl_step);
     return hipGetLastError();
 }
 hipError_t launch_synthetic_actions(const SimState &S, const ObsTable &t, uint32_t seed,
@@ -1367,14 +1389,17 @@ hipError_t launch_synthetic_actions(const SimState &S, const ObsTable &t, uint32
                        seed, step, write_hidden);
     return hipGetLastError();
 }
-hipError_t launch_construct_obs(const SimState &S, const ObsTable &t, int prev, float *out,
-                                uint32_t out_rows, hipStream_t st)
+hipError_t launch_construct_obs(const SimState &S, const ObsTable &t, int prev, int prev_lazy,
+                                float *out, uint32_t out_rows, hipStream_t st)
 {
+    // Prev{Health, Position, Surrounding} left lazy by the shift are the current ones
+    const bool lz = prev && prev_lazy;
     const bool fixd = (S.flags & kFlagFixDepth) != 0;
     const int8_t *sem = prev ? t.psem : t.sem;
     const uint8_t *depth = fixd ? (prev ? t.pdepth : t.depth) : reinterpret_cast<const uint8_t *>(sem);
     hipLaunchKernelGGL(construct_obs_kernel, dim3(4096), dim3(256), 0, st, S.totals, depth, sem,
-                       prev ? t.phealth : t.health, prev ? t.ppos : t.pos, prev ? t.psur : t.sur,
+                       prev && !lz ? t.phealth : t.health, prev && !lz ? t.ppos : t.pos,
+                       prev && !lz ? t.psur : t.sur,
                        out, out_rows);
     return hipGetLastError();
 }

@@ -64,13 +64,17 @@ hipError_t launch_tile_sum(const SimState &S, int parity, hipStream_t st);
 hipError_t launch_world_step(const SimState &S, const ObsTable &cur, int parity, hipStream_t st);
 hipError_t launch_scan(const SimState &S, int parity, hipStream_t st);
 hipError_t launch_export_rows(const SimState &S, const ObsTable &nxt, int init, hipStream_t st);
-hipError_t launch_move(const SimState &S, const ObsTable &cur, const ObsTable &nxt, hipStream_t st);
+hipError_t launch_move(const SimState &S, const ObsTable &cur, const ObsTable &nxt, int prev_lazy,
+                       hipStream_t st);
 hipError_t launch_sensor(const SimState &S, const ObsTable &nxt, hipStream_t st);
-hipError_t launch_shift(const SimState &S, const ObsTable &t, hipStream_t st);
+// shift modes: every Prev* column / Action + HiddenState only (lazy) / the six
+// columns a lazy shift left (materialise)
+constexpr int kShiftAll = 0, kShiftEager = 1, kShiftRest = 2;
+hipError_t launch_shift(const SimState &S, const ObsTable &t, int mode, hipStream_t st);
 hipError_t launch_synthetic_actions(const SimState &S, const ObsTable &t, uint32_t seed,
                                     uint32_t step, int write_hidden, hipStream_t st);
 hipError_t launch_sensor_index(const SimState &S, int32_t *out, hipStream_t st);
-hipError_t launch_construct_obs(const SimState &S, const ObsTable &t, int prev, float *out,
-                                uint32_t out_rows, hipStream_t st);
+hipError_t launch_construct_obs(const SimState &S, const ObsTable &t, int prev, int prev_lazy,
+                                float *out, uint32_t out_rows, hipStream_t st);
 
 }  // namespace mbots

@@ -75,6 +75,8 @@ struct mbots_handle {
     hipStream_t aux = nullptr;        // internal stream of the K3b sensor (forked after K2)
     hipEvent_t ev_join[2] = {nullptr, nullptr};   // K3b of alternate steps done (aux)
     int last_join = -1;               // ev_join of the latest K3b, -1: none pending
+    bool prev_lazy[2] = {false, false};   // table half's six shift-owned Prev* columns are
+                                          // still its current ones (lazy shift, K5)
     uint64_t steps = 0;               // steps run
     hipStream_t last_stream = nullptr;
     bool timing = false;
@@ -193,6 +195,17 @@ hipStream_t as_stream(void *s) { return reinterpret_cast<hipStream_t>(s); }
 int wait_sensor(mbots_handle *h)
 {
     if (h->last_join >= 0) HIP_TRY(hipStreamWaitEvent(h->last_stream, h->ev_join[h->last_join], 0));
+    return MBOTS_OK;
+}
+
+// copy the six Prev* columns a lazy shift left as views of the current ones
+// (on the stream the caller uses next)
+int materialize_prev(mbots_handle *h, hipStream_t st)
+{
+    if (!h->prev_lazy[h->tb]) return MBOTS_OK;
+    HIP_TRY(hipSetDevice(h->device));
+    HIP_TRY(mbots::launch_shift(h->S, h->T[h->tb], mbots::kShiftRest, st));
+    h->prev_lazy[h->tb] = false;
     return MBOTS_OK;
 }
 
@@ -341,7 +354,7 @@ int mbots_create(const mbots_config *cfg_in, mbots_handle **out)
     check(mbots::launch_tile_sum(S, 0, st), "tile_sum_kernel");
     check(mbots::launch_scan(S, 0, st), "scan_kernel");
     check(mbots::launch_export_rows(S, h->T[0], 1, st), "export_rows_kernel(init)");
-    check(mbots::launch_move(S, h->T[1], h->T[0], st), "move_kernel(init)");
+    check(mbots::launch_move(S, h->T[1], h->T[0], 0, st), "move_kernel(init)");
     if (rc == MBOTS_OK) rc = record_totals(h, st);
     check(hipStreamSynchronize(st), "hipStreamSynchronize");
     if (rc != MBOTS_OK) {
@@ -384,6 +397,7 @@ int mbots_step(mbots_handle *h, void *stream)
     const mbots::ObsTable &nxt = h->T[h->tb ^ 1];
     int rc;
     const int par = h->parity;
+    const int lazy = h->prev_lazy[h->tb] ? 1 : 0;
     // K1 reads the finder slots the previous step's sensor wrote, and writes the
     // state half that sensor read; the halves swap after K1.
     if (h->last_join >= 0) HIP_TRY(hipStreamWaitEvent(st, h->ev_join[h->last_join], 0));
@@ -398,7 +412,8 @@ int mbots_step(mbots_handle *h, void *stream)
     if ((rc = timed(h, MBOTS_TK_EXPORT, st,
                     [&] { return mbots::launch_export_rows(h->S, nxt, 0, st); })))
         return rc;
-    if ((rc = timed(h, MBOTS_TK_MOVE, st, [&] { return mbots::launch_move(h->S, cur, nxt, st); })))
+    if ((rc = timed(h, MBOTS_TK_MOVE, st,
+                    [&] { return mbots::launch_move(h->S, cur, nxt, lazy, st); })))
         return rc;
     if ((rc = timed(h, MBOTS_TK_SENSOR, st, [&] { return mbots::launch_sensor(h->S, nxt, st); })))
         return rc;
@@ -417,12 +432,14 @@ int mbots_step(mbots_handle *h, void *stream)
     if ((rc = timed(h, MBOTS_TK_EXPORT, st,
                     [&] { return mbots::launch_export_rows(h->S, nxt, 0, st); })))
         return rc;
-    if ((rc = timed(h, MBOTS_TK_MOVE, st, [&] { return mbots::launch_move(h->S, cur, nxt, st); })))
+    if ((rc = timed(h, MBOTS_TK_MOVE, st,
+                    [&] { return mbots::launch_move(h->S, cur, nxt, lazy, st); })))
         return rc;
 #endif
     ++h->steps;
     h->parity ^= 1;
     h->tb ^= 1;
+    h->prev_lazy[h->tb] = false;   // the move wrote every Prev* column of the new table
     return MBOTS_OK;
 }
 
@@ -432,7 +449,14 @@ int mbots_shift_observations(mbots_handle *h, void *stream)
     HIP_TRY(hipSetDevice(h->device));
     hipStream_t st = as_stream(stream);
     h->last_stream = st;
-    return timed(h, MBOTS_TK_SHIFT, st, [&] { return mbots::launch_shift(h->S, h->T[h->tb], st); });
+    // Action / HiddenState now (the learner overwrites them next); the other six
+    // Prev* columns stay views of the current ones until the next step or an
+    // accessor needs them (K5, lazy shift)
+    const int rc = timed(h, MBOTS_TK_SHIFT, st, [&] {
+        return mbots::launch_shift(h->S, h->T[h->tb], mbots::kShiftEager, st);
+    });
+    if (rc == MBOTS_OK) h->prev_lazy[h->tb] = true;
+    return rc;
 }
 
 int mbots_num_agents(mbots_handle *h, uint32_t *out)
@@ -451,6 +475,13 @@ int mbots_export(mbots_handle *h, int32_t id, mbots_tensor *out)
     uint32_t N = 0;
     int rc = mbots_num_agents(h, &N);
     if (rc) return rc;
+    switch (id) {
+    case MBOTS_EXPORT_PREV_SPECIES: case MBOTS_EXPORT_PREV_POSITION: case MBOTS_EXPORT_PREV_HEALTH:
+    case MBOTS_EXPORT_PREV_SURROUNDING: case MBOTS_EXPORT_PREV_REWARD: case MBOTS_EXPORT_PREV_STATS:
+        if ((rc = materialize_prev(h, h->last_stream))) return rc;
+        break;
+    default: break;
+    }
     const ObsTable &t = h->T[h->tb];
     const bool fixd = (h->cfg.flags & MBOTS_FLAG_FIX_DEPTH_ALIAS) != 0;
     void *p = nullptr;
@@ -549,7 +580,8 @@ int mbots_construct_obs(mbots_handle *h, int32_t prev, float *out, uint64_t out_
     h->last_stream = st;
     int rc;
     if (!prev && (rc = wait_sensor(h))) return rc;   // current semantic rows come from K3b
-    HIP_TRY(mbots::launch_construct_obs(h->S, h->T[h->tb], prev, out, (uint32_t)out_rows, st));
+    HIP_TRY(mbots::launch_construct_obs(h->S, h->T[h->tb], prev, h->prev_lazy[h->tb] ? 1 : 0, out,
+                                        (uint32_t)out_rows, st));
     return MBOTS_OK;
 }
 
@@ -595,6 +627,8 @@ int mbots_save_checkpoint(mbots_handle *h, void *dst, uint64_t bytes)
 {
     if (!h || !dst) return fail(MBOTS_E_INVALID, "null argument");
     HIP_TRY(hipSetDevice(h->device));
+    int rc0 = materialize_prev(h, h->last_stream);
+    if (rc0) return rc0;
     HIP_TRY(hipDeviceSynchronize());   // the sensor's finder / semantic rows included
     int rc = sync_totals(h);
     if (rc) return rc;
@@ -651,6 +685,7 @@ int mbots_load_checkpoint(mbots_handle *h, const void *src, uint64_t bytes)
     h->tb = 0;
     h->parity = 0;
     h->last_join = -1;
+    h->prev_lazy[0] = h->prev_lazy[1] = false;
     h->steps = 1;
     hipStream_t st = nullptr;
     int rc = record_totals(h, st);

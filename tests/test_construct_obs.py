@@ -32,6 +32,11 @@ def test_fused_obs_equals_torch_cat(fix_depth):
                 ref = rollout.construct_obs(sim, s, e, prev=prev)
                 assert torch.equal(_bits(fused[s:e]), _bits(ref)), (t, prev, s, e)
         sim.shift_observations()
+        # after the (lazy) shift: Prev rows read through the current columns
+        fused = sim.construct_obs(True)
+        for s, e in rollout.species_offsets(sim):
+            ref = rollout.construct_obs(sim, s, e, prev=True)
+            assert torch.equal(_bits(fused[s:e]), _bits(ref)), (t, "shifted", s, e)
         sim.write_synthetic_actions(1234, t + 1)
 
 
