@@ -868,14 +868,20 @@ __device__ __forceinline__ void run_survivors(SensorLDS &L, int nf, int a0, int 
                 uint32_t *kr = L.key + ic * kKeyStride;
                 const int kl = k0 + max(c - 1, 0);
                 const float ua = L.u[k0 & 31], ub = L.u[kl & 31];
+                const uint32_t kin = zkey(max0(fwd ? f - 1.0f : -f - 1.0f), order);
+#if MB_ABL & 512
+                const uint32_t ka = kin, kb = kin;
+#else
                 const uint32_t ka = pixel_key(f, l, ua, fwd, order);
                 const uint32_t kb = pixel_key(f, l, ub, fwd, order);
+#endif
                 const uint32_t kf = finder_key(f, l, order);
                 if ((c > 0) & (ka != kNoKey)) atomicMin(&kr[k0], ka);
                 if ((c > 1) & (kb != kNoKey)) atomicMin(&kr[kl], kb);
-                if (fwd & (u1 <= 0.0f) & (u2 >= 0.0f) & (kf != kNoKey)) atomicMin(&kr[kSensor], kf);
-                const uint32_t kin = zkey(max0(fwd ? f - 1.0f : -f - 1.0f), order);
-                for (int k = k0 + 1; k < kl; ++k) atomicMin(&kr[k], kin);
+                // far pair: kf is a key iff l^2 <= 1 and f > 0 (q(0) = C <= 0: the
+                // centre ray lies inside the root interval), no interval test needed
+                if (!(MB_ABL & 1024) && (kf != kNoKey)) atomicMin(&kr[kSensor], kf);
+                if (!(MB_ABL & 256)) for (int k = k0 + 1; k < kl; ++k) atomicMin(&kr[k], kin);
             }
         }
     }
@@ -923,7 +929,10 @@ __device__ __forceinline__ void sensor_prefetch(const SimState &S, uint32_t w, u
 #define MB_SENSOR_WPB 4
 #endif
 constexpr int kSensorWorlds = MB_SENSOR_WPB;   // worlds (waves) per sensor block
-__global__ __launch_bounds__(64 * kSensorWorlds) void sensor_kernel(SimState S, ObsTable nxt)
+#ifndef MB_SENSOR_BLOCKS
+#define MB_SENSOR_BLOCKS 8   // min blocks per CU in the launch bounds: <= 64 VGPRs, 8 waves/SIMD
+#endif
+__global__ __launch_bounds__(64 * kSensorWorlds, MB_SENSOR_BLOCKS) void sensor_kernel(SimState S, ObsTable nxt)
 {
     TL_SCOPE(3, S.tl_step);
     __shared__ SensorLDS lds[kSensorWorlds];
