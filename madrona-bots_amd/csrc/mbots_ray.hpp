@@ -43,14 +43,13 @@ __device__ __forceinline__ float wall_z(float ox, float oy, float dx, float dy)
     return t == 0.0f ? 0.0f : t;
 }
 
-// object at view depth z hides the wall iff z * d < (X - o) per axis
+// object at view depth z hides the wall iff z * d < (X - o) per axis: for
+// d > 0 z * d < hi - o, for d < 0 z * d > lo - o, i.e. z * |d| < o - lo (IEEE
+// products and differences are sign-symmetric, so this is the same predicate)
 __device__ __forceinline__ bool beats_wall(float ox, float oy, float dx, float dy, float z)
 {
-    const float zx = z * dx, zy = z * dy;
-    const bool bx = ((dx > 0.0f) & (zx < kInHiX - ox)) | ((dx < 0.0f) & (zx > kInLo - ox)) |
-                    (dx == 0.0f);
-    const bool by = ((dy > 0.0f) & (zy < kInHiY - oy)) | ((dy < 0.0f) & (zy > kInLo - oy)) |
-                    (dy == 0.0f);
+    const bool bx = (dx == 0.0f) | (z * fabsf(dx) < (dx > 0.0f ? kInHiX - ox : ox - kInLo));
+    const bool by = (dy == 0.0f) | (z * fabsf(dy) < (dy > 0.0f ? kInHiY - oy : oy - kInLo));
     return inside_arena(ox, oy) & bx & by;
 }
 
@@ -65,7 +64,8 @@ __device__ __forceinline__ uint32_t pixel_key(float f, float l, float u, bool fw
     const float A = f * f - 1.0f, B2 = 2.0f * (l * f), C = l * l - 1.0f;
     const float q = (A * u - B2) * u + C;
     const float p = f + u * l;
-    const bool hit = (q <= 0.0f) & ((fwdk & (p > 0.0f)) | (!fwdk & (p < 0.0f)));
+    // ahead of the camera: p > 0 (forward) / p < 0 (backward), i.e. (+-p) > 0
+    const bool hit = (q <= 0.0f) & ((fwdk ? p : -p) > 0.0f);
     const float z = zq(max0(fwdk ? f - 1.0f : -f - 1.0f));
     const bool near = f * f + l * l <= 1.0f;
     const uint32_t key = zkey(near ? 0.0f : z, order);
