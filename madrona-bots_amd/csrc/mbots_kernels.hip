@@ -1018,13 +1018,11 @@ __global__ __launch_bounds__(64 * kSensorWorlds, MB_SENSOR_BLOCKS) void sensor_k
             const int self = a < nc ? nf + ia : -1;
             for (int jb = 0; jb < nobj; jb += G) {
                 const int j = jb + o;
-                bool keep = false;
-                if ((j < nobj) & (j != self) & (a < nc)) {
-                    const float2 p = L.obj[j];
-                    const float vx = p.x - ap.x, vy = p.y - ap.y;
-                    const float f = vx * ah.x + vy * ah.y, l = vx * ah.y - vy * ah.x;   // pair_fl
-                    keep = fabsf(l) <= fabsf(f) + kWedge;
-                }
+                // branch-free: every lane reads a valid object and masks the result
+                const float2 p = L.obj[min(j, nobj - 1)];
+                const float vx = p.x - ap.x, vy = p.y - ap.y;
+                const float f = vx * ah.x + vy * ah.y, l = vx * ah.y - vy * ah.x;   // pair_fl
+                const bool keep = (j < nobj) & (j != self) & (a < nc) & (fabsf(l) <= fabsf(f) + kWedge);
                 const uint64_t m = ballot64(keep);
                 if (keep) L.qcode[nq + (int)rank_below(m)] = (uint32_t)a | ((uint32_t)j << 11);
                 nq += __popcll(m);
