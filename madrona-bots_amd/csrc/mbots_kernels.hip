@@ -868,14 +868,15 @@ __device__ __forceinline__ void run_survivors(SensorLDS &L, int nf, int a0, int 
                 uint32_t *kr = L.key + ic * kKeyStride;
                 const int kl = k0 + max(c - 1, 0);
                 const float ua = L.u[k0 & 31], ub = L.u[kl & 31];
-                const uint32_t kin = zkey(max0(fwd ? f - 1.0f : -f - 1.0f), order);
+                const uint32_t kin = zkey(fwd ? f - 1.0f : -f - 1.0f, order);
 #if MB_ABL & 512
                 const uint32_t ka = kin, kb = kin;
 #else
-                const uint32_t ka = pixel_key(f, l, ua, fwd, order);
-                const uint32_t kb = pixel_key(f, l, ub, fwd, order);
+                const uint32_t ka = far_pixel_key(f, l, ua, fwd, kin);
+                const uint32_t kb = far_pixel_key(f, l, ub, fwd, kin);
 #endif
-                const uint32_t kf = finder_key(f, l, order);
+                // finder ray (u = 0) of a far pair: q(0) = l^2 - 1 <= 0 and f > 0
+                const uint32_t kf = ((l * l - 1.0f <= 0.0f) & fwd) ? kin : kNoKey;
                 if ((c > 0) & (ka != kNoKey)) atomicMin(&kr[k0], ka);
                 if ((c > 1) & (kb != kNoKey)) atomicMin(&kr[kl], kb);
                 // far pair: kf is a key iff l^2 <= 1 and f > 0 (q(0) = C <= 0: the
