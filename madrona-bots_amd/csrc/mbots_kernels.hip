@@ -850,13 +850,16 @@ __device__ __forceinline__ void run_survivors(SensorLDS &L, int nf, int a0, int 
         } else {
             const bool fwd = f > 0.0f;
             const float sq = __builtin_amdgcn_sqrtf(r2 - 1.0f);
-            const float ia = __builtin_amdgcn_rcpf(f * f - 1.0f);
-            const float u1 = (l * f - sq) * ia - kUEps, u2 = (l * f + sq) * ia + kUEps;
-            const float sc = fwd ? 12.0f : 4.0f, kmax = fwd ? 23.0f : 7.0f;
-            const float lo = fmaxf((u1 + 1.0f) * sc - 0.5f, -1.0f);
-            const float hi = fminf((u2 + 1.0f) * sc - 0.5f, kmax + 1.0f);
+            const float lf = l * f;
+            // approximate roots u = (lf -+ sq) / (f^2 - 1), widened by kUEps, in
+            // pixel coordinates s = (u + 1) sc - 0.5 (pixel k at s = k)
+            const float sc = fwd ? 12.0f : 4.0f;
+            const float sia = sc * __builtin_amdgcn_rcpf(f * f - 1.0f);
+            const float lo = (lf - sq) * sia + (fwd ? 12.0f * (1.0f - kUEps) - 0.5f : 4.0f * (1.0f - kUEps) - 0.5f);
+            const float hi = (lf + sq) * sia + (fwd ? 12.0f * (1.0f + kUEps) - 0.5f : 4.0f * (1.0f + kUEps) - 0.5f);
+            const int kmax = fwd ? 23 : 7;
             int k0 = max((int)ceilf(lo), 0);
-            const int k1 = min((int)floorf(hi), (int)kmax);
+            const int k1 = min((int)floorf(hi), kmax);
             const int c = k1 - k0 + 1;
             k0 += fwd ? 0 : 24;
             if (!(MB_ABL & 32)) {
