@@ -873,18 +873,15 @@ __device__ __forceinline__ void run_survivors(SensorLDS &L, int nf, int a0, int 
                 const float ua = L.u[k0 & 31], ub = L.u[kl & 31];
                 const uint32_t kin = zkey(fwd ? f - 1.0f : -f - 1.0f, order);
 #if MB_ABL & 512
-                const uint32_t ka = kin, kb = kin;
+                const bool ha = true, hb = true;
 #else
-                const uint32_t ka = far_pixel_key(f, l, ua, fwd, kin);
-                const uint32_t kb = far_pixel_key(f, l, ub, fwd, kin);
+                const bool ha = far_pixel_hit(f, l, ua, fwd), hb = far_pixel_hit(f, l, ub, fwd);
 #endif
                 // finder ray (u = 0) of a far pair: q(0) = l^2 - 1 <= 0 and f > 0
-                const uint32_t kf = ((l * l - 1.0f <= 0.0f) & fwd) ? kin : kNoKey;
-                if ((c > 0) & (ka != kNoKey)) atomicMin(&kr[k0], ka);
-                if ((c > 1) & (kb != kNoKey)) atomicMin(&kr[kl], kb);
-                // far pair: kf is a key iff l^2 <= 1 and f > 0 (q(0) = C <= 0: the
-                // centre ray lies inside the root interval), no interval test needed
-                if (!(MB_ABL & 1024) && (kf != kNoKey)) atomicMin(&kr[kSensor], kf);
+                const bool hf = (l * l - 1.0f <= 0.0f) & fwd;
+                if ((c > 0) & ha) atomicMin(&kr[k0], kin);
+                if ((c > 1) & hb) atomicMin(&kr[kl], kin);
+                if (!(MB_ABL & 1024) && hf) atomicMin(&kr[kSensor], kin);
                 if (!(MB_ABL & 256)) for (int k = k0 + 1; k < kl; ++k) atomicMin(&kr[k], kin);
             }
         }
@@ -936,6 +933,8 @@ constexpr int kSensorWorlds = MB_SENSOR_WPB;   // worlds (waves) per sensor bloc
 #ifndef MB_SENSOR_BLOCKS
 #define MB_SENSOR_BLOCKS 8   // min blocks per CU in the launch bounds: <= 64 VGPRs, 8 waves/SIMD
 #endif
+// kDepth: fix_depth_alias (a depth byte per pixel besides the semantic one)
+template <bool kDepth>
 __global__ __launch_bounds__(64 * kSensorWorlds, MB_SENSOR_BLOCKS) void sensor_kernel(SimState S, ObsTable nxt)
 {
     TL_SCOPE(3, S.tl_step);
@@ -945,7 +944,7 @@ __global__ __launch_bounds__(64 * kSensorWorlds, MB_SENSOR_BLOCKS) void sensor_k
     const uint32_t w = uniform(blockIdx.x * kSensorWorlds + wv);
     if (w >= S.W) return;
     SensorLDS &L = lds[wv];
-    const bool depth = (S.flags & kFlagFixDepth) != 0;
+    constexpr bool depth = kDepth;
 #ifdef MB_PROF
     unsigned long long prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #endif
@@ -1384,8 +1383,12 @@ hipError_t launch_sensor(const SimState &S, const ObsTable &nxt, hipStream_t st)
     // occupancy experiment: extra dynamic LDS per sensor block
     if (const char *e = getenv("MBOTS_SENSOR_LDS_PAD")) pad = (size_t)atol(e);
 #endif
-    hipLaunchKernelGGL(sensor_kernel, dim3((S.W + kSensorWorlds - 1) / kSensorWorlds),
-                       dim3(64 * kSensorWorlds), pad, st, S, nxt);
+    if (S.flags & kFlagFixDepth)
+        hipLaunchKernelGGL(sensor_kernel<true>, dim3((S.W + kSensorWorlds - 1) / kSensorWorlds),
+                           dim3(64 * kSensorWorlds), pad, st, S, nxt);
+    else
+        hipLaunchKernelGGL(sensor_kernel<false>, dim3((S.W + kSensorWorlds - 1) / kSensorWorlds),
+                           dim3(64 * kSensorWorlds), pad, st, S, nxt);
     return hipGetLastError();
 }
 hipError_t launch_shift(const SimState &S, const ObsTable &t, int mode, hipStream_t st)

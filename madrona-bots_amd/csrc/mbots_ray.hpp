@@ -72,14 +72,14 @@ __device__ __forceinline__ uint32_t pixel_key(float f, float l, float u, bool fw
     return (hit | near) ? key : kNoKey;
 }
 
-// pixel_key for a far pair (f^2 + l^2 > 1, |f| > 1.5): never "near", z > 0.5;
-// `zk` = the pair's key zkey(fwd ? f - 1 : -f - 1, order)
-__device__ __forceinline__ uint32_t far_pixel_key(float f, float l, float u, bool fwdk, uint32_t zk)
+// pixel_key's hit test for a far pair (f^2 + l^2 > 1, |f| > 1.5: never "near";
+// its key is zkey(fwd ? f - 1 : -f - 1, order) on every pixel it hits)
+__device__ __forceinline__ bool far_pixel_hit(float f, float l, float u, bool fwdk)
 {
     const float A = f * f - 1.0f, B2 = 2.0f * (l * f), C = l * l - 1.0f;
     const float q = (A * u - B2) * u + C;
     const float p = f + u * l;
-    return ((q <= 0.0f) & ((fwdk ? p : -p) > 0.0f)) ? zk : kNoKey;
+    return (q <= 0.0f) & ((fwdk ? p : -p) > 0.0f);
 }
 
 // the finder ray (u = 0)

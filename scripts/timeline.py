@@ -5,6 +5,7 @@ goes (kernel spans per stream, idle gaps on the critical path).
     python scripts/timeline.py gpurun_out/prof_r01/run_kernel_trace.csv [last_steps]
 """
 import csv, sys
+import re
 from collections import defaultdict
 
 path = sys.argv[1]
@@ -12,7 +13,7 @@ last = int(sys.argv[2]) if len(sys.argv) > 2 else 20
 rows = []
 with open(path) as f:
     for r in csv.DictReader(f):
-        name = r["Kernel_Name"].split("(")[0].replace("mbots::", "")
+        name = re.sub(r"<.*>", "", r["Kernel_Name"].split("(")[0].split()[-1]).replace("mbots::", "")
         rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), name, r["Queue_Id"]))
 rows.sort()
 steps, cur = [], None

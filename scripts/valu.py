@@ -6,6 +6,7 @@ launches): the sensor's secondary (VALU-issue) roofline in bench.py.
     python scripts/valu.py gpurun_out/<dir> <worlds> <out.json>
 """
 import collections
+import re
 import csv
 import json
 import sys
@@ -13,7 +14,7 @@ import sys
 d, worlds, out = sys.argv[1], int(sys.argv[2]), sys.argv[3]
 vals = collections.defaultdict(lambda: collections.defaultdict(float))
 for r in csv.DictReader(open(f"{d}/run_counter_collection.csv")):
-    k = r["Kernel_Name"].split("(")[0].replace("mbots::", "")
+    k = re.sub(r"<.*>", "", r["Kernel_Name"].split("(")[0].split()[-1]).replace("mbots::", "")
     if k.endswith("_kernel"):
         vals[(r["Counter_Name"], k)][int(r["Dispatch_Id"])] += float(r["Counter_Value"])
 per = {}
