@@ -930,18 +930,32 @@ __device__ __forceinline__ void sensor_prefetch(const SimState &S, uint32_t w, u
 #define MB_SENSOR_WPB 4
 #endif
 constexpr int kSensorWorlds = MB_SENSOR_WPB;   // worlds (waves) per sensor block
+#ifndef MB_SENSOR_SPLIT_MAX
+#define MB_SENSOR_SPLIT_MAX 4096   // world counts up to this use the split sensor
+#endif
+#ifndef MB_SENSOR_SPLIT
+#define MB_SENSOR_SPLIT 4          // waves per world of the split sensor
+#endif
 #ifndef MB_SENSOR_BLOCKS
 #define MB_SENSOR_BLOCKS 8   // min blocks per CU in the launch bounds: <= 64 VGPRs, 8 waves/SIMD
 #endif
-// kDepth: fix_depth_alias (a depth byte per pixel besides the semantic one)
-template <bool kDepth>
+// kDepth: fix_depth_alias (a depth byte per pixel besides the semantic one).
+// kSplit: kSplit waves share one world, each taking every kSplit-th key chunk
+// (each stages its own LDS image of the world).  Used at small world counts
+// (<= 4096), where one wave per world leaves SIMDs idle and the step waits on
+// the latency of one world's serial chunk loop (4 waves per world: step -8 % at
+// 4096 worlds; 2 waves: -5 %; no gain at 8192).
+template <bool kDepth, int kSplit>
 __global__ __launch_bounds__(64 * kSensorWorlds, MB_SENSOR_BLOCKS) void sensor_kernel(SimState S, ObsTable nxt)
 {
     TL_SCOPE(3, S.tl_step);
     __shared__ SensorLDS lds[kSensorWorlds];
     const uint32_t wv = threadIdx.x >> 6;
     const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t w = uniform(blockIdx.x * kSensorWorlds + wv);
+    static_assert(kSensorWorlds % kSplit == 0, "split must divide the block's waves");
+    const uint32_t w = uniform(blockIdx.x * (kSensorWorlds / kSplit) + wv / kSplit);
+    constexpr int kChunkStep = kKeyAgents * kSplit;
+    const int kChunk0 = (int)(wv % kSplit) * kKeyAgents;
     if (w >= S.W) return;
     SensorLDS &L = lds[wv];
     constexpr bool depth = kDepth;
@@ -1004,7 +1018,7 @@ __global__ __launch_bounds__(64 * kSensorWorlds, MB_SENSOR_BLOCKS) void sensor_k
     wave_sync();
     PROF_ADD(0, PROF_NOW() - t_start);
 
-    for (int a0 = 0; a0 < n; a0 += kKeyAgents) {
+    for (int a0 = kChunk0; a0 < n; a0 += kChunkStep) {
         const int nc = min(kKeyAgents, n - a0);
         for (int q = lane; q < nc * kKeyStride; q += 64) L.key[q] = kNoKey;
         wave_sync();
@@ -1383,12 +1397,18 @@ hipError_t launch_sensor(const SimState &S, const ObsTable &nxt, hipStream_t st)
     // occupancy experiment: extra dynamic LDS per sensor block
     if (const char *e = getenv("MBOTS_SENSOR_LDS_PAD")) pad = (size_t)atol(e);
 #endif
-    if (S.flags & kFlagFixDepth)
-        hipLaunchKernelGGL(sensor_kernel<true>, dim3((S.W + kSensorWorlds - 1) / kSensorWorlds),
-                           dim3(64 * kSensorWorlds), pad, st, S, nxt);
-    else
-        hipLaunchKernelGGL(sensor_kernel<false>, dim3((S.W + kSensorWorlds - 1) / kSensorWorlds),
-                           dim3(64 * kSensorWorlds), pad, st, S, nxt);
+    const bool fixd = (S.flags & kFlagFixDepth) != 0;
+    const dim3 blk(64 * kSensorWorlds);
+    if (S.W <= (uint32_t)MB_SENSOR_SPLIT_MAX) {   // small: MB_SENSOR_SPLIT waves per world
+        constexpr int kWpb = kSensorWorlds / MB_SENSOR_SPLIT;
+        const dim3 grid((S.W + kWpb - 1) / kWpb);
+        if (fixd) hipLaunchKernelGGL((sensor_kernel<true, MB_SENSOR_SPLIT>), grid, blk, pad, st, S, nxt);
+        else hipLaunchKernelGGL((sensor_kernel<false, MB_SENSOR_SPLIT>), grid, blk, pad, st, S, nxt);
+    } else {
+        const dim3 grid((S.W + kSensorWorlds - 1) / kSensorWorlds);
+        if (fixd) hipLaunchKernelGGL((sensor_kernel<true, 1>), grid, blk, pad, st, S, nxt);
+        else hipLaunchKernelGGL((sensor_kernel<false, 1>), grid, blk, pad, st, S, nxt);
+    }
     return hipGetLastError();
 }
 hipError_t launch_shift(const SimState &S, const ObsTable &t, int mode, hipStream_t st)
