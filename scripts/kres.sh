@@ -15,7 +15,7 @@ for blk in meta.split('\n  - ')[1:]:
     if not m:
         continue
     g = lambda k: (re.search(r'\.' + k + r':\s+(\S+)', blk) or [None, '-'])[1]
-    print(f"{m.group(1).split('E')[0][8:]:28s} vgpr {g('vgpr_count'):>4} sgpr {g('sgpr_count'):>4} "
+    print(f"{m.group(1)[8:40]:32s} vgpr {g('vgpr_count'):>4} sgpr {g('sgpr_count'):>4} "
           f"lds {g('group_segment_fixed_size'):>6} spill {g('vgpr_spill_count')}/{g('sgpr_spill_count')}")
 PY
 rm -rf $d
