@@ -60,6 +60,24 @@ def load_traffic(worlds):
     return best
 
 
+def load_kernel_stats():
+    """Average duration (ms) per kernel from the committed rocprofv3 --stats
+    summary (profiles/*_kernel_stats.csv, the latest), or {}."""
+    import csv
+    import glob
+    import re
+    files = sorted(f for f in glob.glob(os.path.join(ROOT, "profiles", "r*_kernel_stats.csv"))
+                   if re.fullmatch(r"r\d+_kernel_stats\.csv", os.path.basename(f)))
+    if not files:
+        return {}, None
+    out = {}
+    with open(files[-1]) as f:
+        for r in csv.DictReader(f):
+            name = re.sub(r"<.*>", "", r["Name"].split("(")[0].split()[-1]).replace("mbots::", "")
+            out[name] = float(r["AverageNs"]) * 1e-6
+    return out, os.path.relpath(files[-1], ROOT)
+
+
 def load_profile(suffix, worlds):
     """profiles/*_<suffix>.json recorded at `worlds` (the latest), or None."""
     import glob
@@ -296,6 +314,24 @@ def main():
             out["kernel_ms"] = {k: round(v, 5) for k, v in per.items() if v}
             out["kernel_ms_note"] = ("HIP events around each kernel in an untimed pass after "
                                      "the timed region (overlapped schedule)")
+            # per-kernel HBM rate: PMC bytes per launch / event span in the
+            # overlapped schedule, beside rocprofv3's average for the same kernel
+            kmap = {"world_step": "world_step_kernel", "scan": "scan_kernel",
+                    "export": "export_rows_kernel", "move": "move_kernel",
+                    "sensor": "sensor_kernel", "shift": "shift_kernel",
+                    "actions": "synthetic_actions_kernel"}
+            if tr:
+                kst, kst_src = load_kernel_stats()
+                kh = {}
+                for k, kn in kmap.items():
+                    b = tr[1]["kernels"].get(kn, {}).get("hbm_bytes_per_launch")
+                    if b and per.get(k):
+                        gbs = b / (per[k] * 1e-3) / 1e9
+                        kh[k] = {"hbm_bytes": b, "event_ms": round(per[k], 5),
+                                 "rocprof_avg_ms": round(kst[kn], 5) if kn in kst else None,
+                                 "GBps": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4)}
+                out["kernel_hbm"] = kh
+                out["kernel_hbm_sources"] = {"bytes": tr[0], "rocprof": kst_src}
             vp = load_profile("valu", W)
             sens = vp[1]["kernels"].get("sensor_kernel") if vp else None
             if sens and per.get("sensor"):
