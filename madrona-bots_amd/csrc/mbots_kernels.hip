@@ -193,6 +193,11 @@ __device__ void world_step(SimState &S, const ObsTable &cur, WorldLDS &L, uint32
     // row_hi): only the slot's own lane reads them (action fetch, compaction).
     int2 pa0 = make_int2(0, 0), pa1 = pa0, pa2 = pa0;
     int32_t row_lo = -1, row_hi = -1;
+    // per-world records: issued with the first batch (none depends on n0)
+    const uint64_t food_rec = lane < kNumChunks ? S.food[(size_t)w * kNumChunks + lane] : 0ull;
+    const uint2 key = S.key[w];
+    uint32_t ctr = S.ctr[w];
+    int32_t cur_food = S.cur_food[w];
     {
         // slots < 64: loaded without waiting for n0 (slots past n0 are stale
         // and dropped), so only the action rows wait on a second round trip
@@ -236,13 +241,10 @@ __device__ void world_step(SimState &S, const ObsTable &cur, WorldLDS &L, uint32
         L.finder[i] = (int8_t)S.finder[base + i];
         L.flags[i] = (uint8_t)F_ALIVE;
     }
-    if (lane < kNumChunks) food_unpack(S.food[(size_t)w * kNumChunks + lane], &L.food[lane * kMaxPkg]);
+    if (lane < kNumChunks) food_unpack(food_rec, &L.food[lane * kMaxPkg]);
     if (lane < kNumChunks) L.chunk[lane] = 0u;   // resetChunkInfoSystem
     if (lane < kNumSpecies) { L.cnt[lane] = 0u; L.hsum[lane] = 0u; L.scount[lane] = 0; }
     if (lane == 0) L.consumed = 0;
-    const uint2 key = S.key[w];
-    uint32_t ctr = S.ctr[w];
-    int32_t cur_food = S.cur_food[w];
     wave_sync();
     KPROF(0);
 
@@ -908,14 +910,18 @@ struct SensorPrefetch {
     float x, y, rw, rz;        // lane < min(n, 64): agent slot `lane`
     int32_t sp;
     int n;
+    int4 rb;                   // row_base[w]
 };
 
 __device__ __forceinline__ void sensor_prefetch(const SimState &S, uint32_t w, uint32_t lane,
                                                 SensorPrefetch &p)
 {
     p.n = uniform(S.n[w]);
+    p.rb = reinterpret_cast<const int4 *>(S.row_base)[w];
     p.food = lane < kNumChunks ? S.food[(size_t)w * kNumChunks + lane] : 0ull;
-    if ((int)lane < p.n) {   // slots [0, n) (rows past n are stale)
+    // slots [0, min(cap, 64)), loaded without waiting for n (rows past n are
+    // stale and never used)
+    if (lane < S.cap) {
         const size_t i = (size_t)w * S.cap + lane;
         p.x = S.x[i];
         p.y = S.y[i];
@@ -986,7 +992,7 @@ __global__ __launch_bounds__(64 * kSensorWorlds, MB_SENSOR_BLOCKS) void sensor_k
     // K3a): row_base[w][species] + rank among the world's slots of that
     // species.  They stay in registers: lane s holds slot s (row_lo) and 64 + s
     // (row_hi).
-    const int4 rb = reinterpret_cast<const int4 *>(S.row_base)[w];
+    const int4 rb = cur.rb;
     int row_lo, row_hi = 0;
     int c1, c2, c3, c4;
     {

@@ -1,13 +1,12 @@
 #!/bin/bash
-# GPU side of an A/B run: time every build_var/*.so (and the default build).
+# Same-box A/B: the default build vs build_var/libmbots_*.so, interleaved, N rounds.
+#   ab.sh [rounds] [kbench args...]
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-mkdir -p gpurun_out
-: > gpurun_out/ab.jsonl
-shopt -s nullglob
-for lib in madrona-bots_amd/madrona_bots/libmbots.so build_var/*.so; do
-  MBOTS_LIB=$lib timeout -k 10 240 python scripts/kbench.py "$@" >> gpurun_out/ab.jsonl 2> gpurun_out/ab_err.log
-  rc=$?
-  if [ $rc -ne 0 ]; then echo "abort: $lib rc=$rc"; tail -5 gpurun_out/ab_err.log; exit $rc; fi
+n=${1:-2}; shift
+for r in $(seq $n); do
+  timeout -k 10 120 python scripts/kbench.py --no-kernel-timing "$@" || exit 1
+  for lib in build_var/libmbots_*.so; do
+    MBOTS_LIB=$lib timeout -k 10 120 python scripts/kbench.py --no-kernel-timing "$@" || exit 1
+  done
 done
-cat gpurun_out/ab.jsonl
