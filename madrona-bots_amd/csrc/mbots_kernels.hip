@@ -61,6 +61,64 @@ struct TLScope {
 constexpr int kWorldsPerBlock = 4;
 constexpr int kTileWorlds = 1024;             // worlds per scan tile (K2 block)
 
+#ifndef MB_NT
+#define MB_NT 35  // non-temporal stores: 1 K4, 2 K5, 4 K3a, 8 sensor output, 16 K4 but Action/Hidden;
+                  // non-temporal loads: 32 K4 sources, 64 K5 sources
+#endif
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void st_stream(uint32_t *p, uint32_t v, bool nt)
+{
+    if (nt) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+__device__ __forceinline__ void st_stream(int32_t *p, int32_t v, bool nt)
+{
+    if (nt) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+__device__ __forceinline__ void st_stream(float *p, float v, bool nt)
+{
+    if (nt) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+__device__ __forceinline__ void st_stream(uint2 *p, uint2 v, bool nt)
+{
+    if (nt) __builtin_nontemporal_store(u32x2{v.x, v.y}, reinterpret_cast<u32x2 *>(p));
+    else *p = v;
+}
+__device__ __forceinline__ void st_stream(float2 *p, float2 v, bool nt)
+{
+    st_stream(reinterpret_cast<uint2 *>(p), make_uint2(__float_as_uint(v.x), __float_as_uint(v.y)), nt);
+}
+__device__ __forceinline__ void st_stream(uint4 *p, uint4 v, bool nt)
+{
+    if (nt) __builtin_nontemporal_store(u32x4{v.x, v.y, v.z, v.w}, reinterpret_cast<u32x4 *>(p));
+    else *p = v;
+}
+__device__ __forceinline__ void st_stream(int4 *p, int4 v, bool nt)
+{
+    st_stream(reinterpret_cast<uint4 *>(p), make_uint4(v.x, v.y, v.z, v.w), nt);
+}
+// loads of data read once
+__device__ __forceinline__ uint32_t ld_stream(const uint32_t *p, bool nt)
+{
+    return nt ? __builtin_nontemporal_load(p) : *p;
+}
+__device__ __forceinline__ uint2 ld_stream(const uint2 *p, bool nt)
+{
+    if (!nt) return *p;
+    const u32x2 v = __builtin_nontemporal_load(reinterpret_cast<const u32x2 *>(p));
+    return make_uint2(v.x, v.y);
+}
+__device__ __forceinline__ uint4 ld_stream(const uint4 *p, bool nt)
+{
+    if (!nt) return *p;
+    const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(p));
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+
+
 // ---------------------------------------------------------------------------
 // Food packages: HBM keeps one 8-byte record per chunk (5 x (x | y << 4) bytes,
 // live mask in byte 5: kMaxFoodPerPackage = 1, so numFood is a bit);
@@ -660,13 +718,14 @@ __global__ __launch_bounds__(256) void export_rows_kernel(SimState S, ObsTable n
         const uint32_t st = init ? 0u : S.stats[base + i];
         S.src_of[r] = S.obsrow[base + i];
         S.obsrow[base + i] = row;
-        nxt.species[r] = sp;
-        reinterpret_cast<float2 *>(nxt.pos)[r] = make_float2(x, y);
-        nxt.health[r] = h;
-        reinterpret_cast<float2 *>(nxt.sur)[r] = make_float2(s0, s1);
+        constexpr bool nt = (MB_NT & 4) != 0;
+        st_stream(nxt.species + r, sp, nt);
+        st_stream(reinterpret_cast<float2 *>(nxt.pos) + r, make_float2(x, y), nt);
+        st_stream(nxt.health + r, h, nt);
+        st_stream(reinterpret_cast<float2 *>(nxt.sur) + r, make_float2(s0, s1), nt);
         const int4 stv = make_int4((int)(st & 1u), (int)((st >> 1) & 1u), (int)((st >> 2) & 1u),
                                    (int)((st >> 3) & 1u));
-        reinterpret_cast<int4 *>(nxt.stats)[r] = stv;
+        st_stream(reinterpret_cast<int4 *>(nxt.stats) + r, stv, nt);
         float rv = 0.0f;
         if (!init) {
             float sr;
@@ -677,7 +736,7 @@ __global__ __launch_bounds__(256) void export_rows_kernel(SimState S, ObsTable n
             if (stv.w) rv += 10.0f;
             if (stv.y) rv += 15.0f;
         }
-        nxt.reward[r] = rv;
+        st_stream(nxt.reward + r, rv, nt);
     }
 }
 
@@ -705,11 +764,11 @@ struct MoveArgs {
 };
 
 template <typename T>
-__device__ __forceinline__ void move_item(const MoveSeg &sg, uint32_t idx, int32_t o, uint32_t part)
+__device__ __forceinline__ void move_item(const MoveSeg &sg, uint32_t idx, int32_t o, uint32_t part, bool nt)
 {
     T v{};
-    if (o >= 0) v = reinterpret_cast<const T *>(sg.src)[(size_t)o * sg.ipr + part];
-    reinterpret_cast<T *>(sg.dst)[idx] = v;
+    if (o >= 0) v = ld_stream(reinterpret_cast<const T *>(sg.src) + (size_t)o * sg.ipr + part, (MB_NT & 32) != 0);
+    st_stream(reinterpret_cast<T *>(sg.dst) + idx, v, nt);
 }
 
 __global__ __launch_bounds__(256) void move_kernel(const uint32_t *totals, const int32_t *src_of,
@@ -720,6 +779,8 @@ __global__ __launch_bounds__(256) void move_kernel(const uint32_t *totals, const
     const MoveSeg &sg = args.seg[blockIdx.y];
     const uint32_t items = N * sg.ipr;
     const uint32_t stride = gridDim.x * blockDim.x;
+    // segments 0, 1 are Action / HiddenState, which the shift reads next
+    const bool nt = (MB_NT & 1) || ((MB_NT & 16) && blockIdx.y >= 2);
     for (uint32_t idx = blockIdx.x * blockDim.x + threadIdx.x; idx < items; idx += stride) {
         uint32_t r = idx, part = 0;
         if (sg.ipr == 2) { r = idx >> 1; part = idx & 1u; }
@@ -728,12 +789,12 @@ __global__ __launch_bounds__(256) void move_kernel(const uint32_t *totals, const
         const int32_t o = src_of[r];
         if (sg.width == 16 && sg.xform) {
             uint4 v = make_uint4(0u, 0u, 0u, 0u);
-            if (o >= 0) v = reinterpret_cast<const uint4 *>(sg.src)[o];
+            if (o >= 0) v = ld_stream(reinterpret_cast<const uint4 *>(sg.src) + o, (MB_NT & 32) != 0);
             v.y = v.x;
-            reinterpret_cast<uint4 *>(sg.dst)[idx] = v;
-        } else if (sg.width == 16) move_item<uint4>(sg, idx, o, part);
-        else if (sg.width == 8) move_item<uint2>(sg, idx, o, part);
-        else move_item<uint32_t>(sg, idx, o, part);
+            st_stream(reinterpret_cast<uint4 *>(sg.dst) + idx, v, nt);
+        } else if (sg.width == 16) move_item<uint4>(sg, idx, o, part, nt);
+        else if (sg.width == 8) move_item<uint2>(sg, idx, o, part, nt);
+        else move_item<uint32_t>(sg, idx, o, part, nt);
     }
 }
 
@@ -1098,8 +1159,9 @@ __global__ __launch_bounds__(64 * kSensorWorlds, MB_SENSOR_BLOCKS) void sensor_k
                 }
             }
             if (ci < nc) {
-                reinterpret_cast<uint32_t *>(nxt.sem + (size_t)r * kSensor)[g] = semv;
-                if (depth) reinterpret_cast<uint32_t *>(nxt.depth + (size_t)r * kSensor)[g] = depv;
+                constexpr bool nt = (MB_NT & 8) != 0;
+                st_stream(reinterpret_cast<uint32_t *>(nxt.sem + (size_t)r * kSensor) + g, semv, nt);
+                if (depth) st_stream(reinterpret_cast<uint32_t *>(nxt.depth + (size_t)r * kSensor) + g, depv, nt);
             }
         }
         if ((int)lane < nc) {
@@ -1245,9 +1307,9 @@ __global__ __launch_bounds__(256) void shift_kernel(const uint32_t *totals, ObsT
         else if (g < e5) { src = (const uint4 *)t.action; dst = (uint4 *)t.paction; k = g - e4; }
         else if (g < e6) { src = (const uint4 *)t.stats; dst = (uint4 *)t.pstats; k = g - e5; }
         else { src = (const uint4 *)t.hidden; dst = (uint4 *)t.phidden; k = g - e6; }
-        uint4 v = src[k];
+        uint4 v = ld_stream(src + k, (MB_NT & 64) != 0);
         if (g >= e5 && g < e6) v.y = v.x;
-        dst[k] = v;
+        st_stream(dst + k, v, (MB_NT & 2) != 0);
     }
 }
 
