@@ -73,7 +73,7 @@ def load_kernel_stats():
     out = {}
     with open(files[-1]) as f:
         for r in csv.DictReader(f):
-            name = re.sub(r"<.*>", "", r["Name"].split("(")[0].split()[-1]).replace("mbots::", "")
+            name = re.sub(r"<.*>", "", r["Name"].split("(")[0]).split()[-1].replace("mbots::", "")
             out[name] = float(r["AverageNs"]) * 1e-6
     return out, os.path.relpath(files[-1], ROOT)
 

@@ -6,7 +6,7 @@ root = sys.argv[1]
 rows = collections.defaultdict(lambda: collections.defaultdict(list))
 for f in sorted(glob.glob(f"{root}_p*/run_counter_collection.csv")):
     for r in csv.DictReader(open(f)):
-        k = re.sub(r"<.*>", "", r["Kernel_Name"].split("(")[0].split()[-1]).replace("mbots::", "")
+        k = re.sub(r"<.*>", "", r["Kernel_Name"].split("(")[0]).split()[-1].replace("mbots::", "")
         rows[k][r["Counter_Name"]].append((int(r["Dispatch_Id"]), float(r["Counter_Value"])))
 for k, cs in rows.items():
     print(k)

@@ -13,7 +13,7 @@ last = int(sys.argv[2]) if len(sys.argv) > 2 else 20
 rows = []
 with open(path) as f:
     for r in csv.DictReader(f):
-        name = re.sub(r"<.*>", "", r["Kernel_Name"].split("(")[0].split()[-1]).replace("mbots::", "")
+        name = re.sub(r"<.*>", "", r["Kernel_Name"].split("(")[0]).split()[-1].replace("mbots::", "")
         rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), name, r["Queue_Id"]))
 rows.sort()
 steps, cur = [], None

@@ -20,7 +20,7 @@ vals = collections.defaultdict(lambda: collections.defaultdict(float))
 names = {}
 for f in sorted(glob.glob(f"{root}_p*/run_counter_collection.csv")):
     for r in csv.DictReader(open(f)):
-        k = re.sub(r"<.*>", "", r["Kernel_Name"].split("(")[0].split()[-1]).replace("mbots::", "")
+        k = re.sub(r"<.*>", "", r["Kernel_Name"].split("(")[0]).split()[-1].replace("mbots::", "")
         if not k.endswith("_kernel"):
             continue
         d = int(r["Dispatch_Id"])

@@ -14,7 +14,7 @@ import sys
 d, worlds, out = sys.argv[1], int(sys.argv[2]), sys.argv[3]
 vals = collections.defaultdict(lambda: collections.defaultdict(float))
 for r in csv.DictReader(open(f"{d}/run_counter_collection.csv")):
-    k = re.sub(r"<.*>", "", r["Kernel_Name"].split("(")[0].split()[-1]).replace("mbots::", "")
+    k = re.sub(r"<.*>", "", r["Kernel_Name"].split("(")[0]).split()[-1].replace("mbots::", "")
     if k.endswith("_kernel"):
         vals[(r["Counter_Name"], k)][int(r["Dispatch_Id"])] += float(r["Counter_Value"])
 per = {}
