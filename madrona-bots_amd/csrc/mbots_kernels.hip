@@ -779,7 +779,8 @@ __global__ __launch_bounds__(256) void move_kernel(const uint32_t *totals, const
     const MoveSeg &sg = args.seg[blockIdx.y];
     const uint32_t items = N * sg.ipr;
     const uint32_t stride = gridDim.x * blockDim.x;
-    // segments 0, 1 are Action / HiddenState, which the shift reads next
+    // (MB_NT & 16: segments 0, 1 -- Action / HiddenState, which the shift reads
+    // next -- keep plain stores)
     const bool nt = (MB_NT & 1) || ((MB_NT & 16) && blockIdx.y >= 2);
     for (uint32_t idx = blockIdx.x * blockDim.x + threadIdx.x; idx < items; idx += stride) {
         uint32_t r = idx, part = 0;
@@ -1433,7 +1434,7 @@ hipError_t launch_export_rows(const SimState &S, const ObsTable &nxt, int init, 
     return hipGetLastError();
 }
 hipError_t launch_move(const SimState &S, const ObsTable &cur, const ObsTable &nxt, int prev_lazy,
-                       hipStream_t st)
+                       int parts, hipStream_t st)
 {
     MoveArgs m{};
     int k = 0;
@@ -1442,18 +1443,23 @@ hipError_t launch_move(const SimState &S, const ObsTable &cur, const ObsTable &n
     };
     // after a lazy shift the six Prev* columns it left are the current ones
     const bool lz = prev_lazy != 0;
-    add(nxt.action, cur.action, 8, 3);
-    add(nxt.hidden, cur.hidden, 16, 4);
-    add(nxt.pspecies, lz ? cur.species : cur.pspecies, 4, 1);
-    add(nxt.ppos, lz ? cur.pos : cur.ppos, 8, 1);
-    add(nxt.phealth, lz ? cur.health : cur.phealth, 4, 1);
-    add(nxt.psur, lz ? cur.sur : cur.psur, 8, 1);
-    add(nxt.preward, lz ? cur.reward : cur.preward, 4, 1);
-    add(nxt.paction, cur.paction, 8, 3);
-    add(nxt.pstats, lz ? cur.stats : cur.pstats, 16, 1, lz ? 1u : 0u);
-    add(nxt.phidden, cur.phidden, 16, 4);
-    add(nxt.psem, cur.sem, 16, 2);                   // prev sensor <- last step's sensor
-    if (S.flags & kFlagFixDepth) add(nxt.pdepth, cur.depth, 16, 2);
+    if (parts & kMoveMain) {
+        add(nxt.action, cur.action, 8, 3);
+        add(nxt.hidden, cur.hidden, 16, 4);
+        add(nxt.pspecies, lz ? cur.species : cur.pspecies, 4, 1);
+        add(nxt.ppos, lz ? cur.pos : cur.ppos, 8, 1);
+        add(nxt.phealth, lz ? cur.health : cur.phealth, 4, 1);
+        add(nxt.psur, lz ? cur.sur : cur.psur, 8, 1);
+        add(nxt.preward, lz ? cur.reward : cur.preward, 4, 1);
+        add(nxt.pstats, lz ? cur.stats : cur.pstats, 16, 1, lz ? 1u : 0u);
+        add(nxt.psem, cur.sem, 16, 2);                   // prev sensor <- last step's sensor
+        if (S.flags & kFlagFixDepth) add(nxt.pdepth, cur.depth, 16, 2);
+    }
+    if (parts & kMovePrevAH) {
+        add(nxt.paction, cur.paction, 8, 3);
+        add(nxt.phidden, cur.phidden, 16, 4);
+    }
+    if (k == 0) return hipSuccess;
     m.nseg = k;
     hipLaunchKernelGGL(move_kernel, dim3(512, k), dim3(256), 0, st, S.totals, S.src_of, m, S.tl_step);
     return hipGetLastError();

@@ -64,8 +64,11 @@ hipError_t launch_tile_sum(const SimState &S, int parity, hipStream_t st);
 hipError_t launch_world_step(const SimState &S, const ObsTable &cur, int parity, hipStream_t st);
 hipError_t launch_scan(const SimState &S, int parity, hipStream_t st);
 hipError_t launch_export_rows(const SimState &S, const ObsTable &nxt, int init, hipStream_t st);
+// K4 parts: every moved column but PrevAction / PrevHiddenState, and those two
+// (deferred: a shift overwrites them, DESIGN.md "Deferred prev moves")
+constexpr int kMoveMain = 1, kMovePrevAH = 2, kMoveAll = 3;
 hipError_t launch_move(const SimState &S, const ObsTable &cur, const ObsTable &nxt, int prev_lazy,
-                       hipStream_t st);
+                       int parts, hipStream_t st);
 hipError_t launch_sensor(const SimState &S, const ObsTable &nxt, hipStream_t st);
 // shift modes: every Prev* column / Action + HiddenState only (lazy) / the six
 // columns a lazy shift left (materialise)

@@ -75,6 +75,8 @@ struct mbots_handle {
     hipStream_t aux = nullptr;        // internal stream of the K3b sensor (forked after K2)
     hipEvent_t ev_join[2] = {nullptr, nullptr};   // K3b of alternate steps done (aux)
     int last_join = -1;               // ev_join of the latest K3b, -1: none pending
+    bool ah_pending[2] = {false, false};  // table half's PrevAction / PrevHiddenState not yet
+                                          // moved from the other half (deferred K4 part)
     bool prev_lazy[2] = {false, false};   // table half's six shift-owned Prev* columns are
                                           // still its current ones (lazy shift, K5)
     uint64_t steps = 0;               // steps run
@@ -206,6 +208,18 @@ int materialize_prev(mbots_handle *h, hipStream_t st)
     HIP_TRY(hipSetDevice(h->device));
     HIP_TRY(mbots::launch_shift(h->S, h->T[h->tb], mbots::kShiftRest, st));
     h->prev_lazy[h->tb] = false;
+    return MBOTS_OK;
+}
+
+// the deferred K4 part: PrevAction / PrevHiddenState of the current half from
+// the other half, along the last step's src_of (both intact until the next
+// step's K3a / K4)
+int materialize_prev_ah(mbots_handle *h, hipStream_t st)
+{
+    if (!h->ah_pending[h->tb]) return MBOTS_OK;
+    HIP_TRY(hipSetDevice(h->device));
+    HIP_TRY(mbots::launch_move(h->S, h->T[h->tb ^ 1], h->T[h->tb], 0, mbots::kMovePrevAH, st));
+    h->ah_pending[h->tb] = false;
     return MBOTS_OK;
 }
 
@@ -354,7 +368,7 @@ int mbots_create(const mbots_config *cfg_in, mbots_handle **out)
     check(mbots::launch_tile_sum(S, 0, st), "tile_sum_kernel");
     check(mbots::launch_scan(S, 0, st), "scan_kernel");
     check(mbots::launch_export_rows(S, h->T[0], 1, st), "export_rows_kernel(init)");
-    check(mbots::launch_move(S, h->T[1], h->T[0], 0, st), "move_kernel(init)");
+    check(mbots::launch_move(S, h->T[1], h->T[0], 0, mbots::kMoveAll, st), "move_kernel(init)");
     if (rc == MBOTS_OK) rc = record_totals(h, st);
     check(hipStreamSynchronize(st), "hipStreamSynchronize");
     if (rc != MBOTS_OK) {
@@ -398,6 +412,8 @@ int mbots_step(mbots_handle *h, void *stream)
     int rc;
     const int par = h->parity;
     const int lazy = h->prev_lazy[h->tb] ? 1 : 0;
+    // no shift since the last step: its deferred Prev moves first
+    if ((rc = materialize_prev_ah(h, st))) return rc;
     // K1 reads the finder slots the previous step's sensor wrote, and writes the
     // state half that sensor read; the halves swap after K1.
     if (h->last_join >= 0) HIP_TRY(hipStreamWaitEvent(st, h->ev_join[h->last_join], 0));
@@ -413,7 +429,7 @@ int mbots_step(mbots_handle *h, void *stream)
                     [&] { return mbots::launch_export_rows(h->S, nxt, 0, st); })))
         return rc;
     if ((rc = timed(h, MBOTS_TK_MOVE, st,
-                    [&] { return mbots::launch_move(h->S, cur, nxt, lazy, st); })))
+                    [&] { return mbots::launch_move(h->S, cur, nxt, lazy, mbots::kMoveMain, st); })))
         return rc;
     if ((rc = timed(h, MBOTS_TK_SENSOR, st, [&] { return mbots::launch_sensor(h->S, nxt, st); })))
         return rc;
@@ -433,13 +449,14 @@ int mbots_step(mbots_handle *h, void *stream)
                     [&] { return mbots::launch_export_rows(h->S, nxt, 0, st); })))
         return rc;
     if ((rc = timed(h, MBOTS_TK_MOVE, st,
-                    [&] { return mbots::launch_move(h->S, cur, nxt, lazy, st); })))
+                    [&] { return mbots::launch_move(h->S, cur, nxt, lazy, mbots::kMoveMain, st); })))
         return rc;
 #endif
     ++h->steps;
     h->parity ^= 1;
     h->tb ^= 1;
     h->prev_lazy[h->tb] = false;   // the move wrote every Prev* column of the new table
+    h->ah_pending[h->tb] = true;   // ... but PrevAction / PrevHiddenState (deferred)
     return MBOTS_OK;
 }
 
@@ -455,7 +472,10 @@ int mbots_shift_observations(mbots_handle *h, void *stream)
     const int rc = timed(h, MBOTS_TK_SHIFT, st, [&] {
         return mbots::launch_shift(h->S, h->T[h->tb], mbots::kShiftEager, st);
     });
-    if (rc == MBOTS_OK) h->prev_lazy[h->tb] = true;
+    if (rc == MBOTS_OK) {
+        h->prev_lazy[h->tb] = true;
+        h->ah_pending[h->tb] = false;   // the shift wrote PrevAction / PrevHiddenState
+    }
     return rc;
 }
 
@@ -479,6 +499,9 @@ int mbots_export(mbots_handle *h, int32_t id, mbots_tensor *out)
     case MBOTS_EXPORT_PREV_SPECIES: case MBOTS_EXPORT_PREV_POSITION: case MBOTS_EXPORT_PREV_HEALTH:
     case MBOTS_EXPORT_PREV_SURROUNDING: case MBOTS_EXPORT_PREV_REWARD: case MBOTS_EXPORT_PREV_STATS:
         if ((rc = materialize_prev(h, h->last_stream))) return rc;
+        break;
+    case MBOTS_EXPORT_PREV_ACTION: case MBOTS_EXPORT_PREV_HIDDEN_STATE:
+        if ((rc = materialize_prev_ah(h, h->last_stream))) return rc;
         break;
     default: break;
     }
@@ -628,6 +651,7 @@ int mbots_save_checkpoint(mbots_handle *h, void *dst, uint64_t bytes)
     if (!h || !dst) return fail(MBOTS_E_INVALID, "null argument");
     HIP_TRY(hipSetDevice(h->device));
     int rc0 = materialize_prev(h, h->last_stream);
+    if (!rc0) rc0 = materialize_prev_ah(h, h->last_stream);
     if (rc0) return rc0;
     HIP_TRY(hipDeviceSynchronize());   // the sensor's finder / semantic rows included
     int rc = sync_totals(h);
@@ -686,6 +710,7 @@ int mbots_load_checkpoint(mbots_handle *h, const void *src, uint64_t bytes)
     h->parity = 0;
     h->last_join = -1;
     h->prev_lazy[0] = h->prev_lazy[1] = false;
+    h->ah_pending[0] = h->ah_pending[1] = false;
     h->steps = 1;
     hipStream_t st = nullptr;
     int rc = record_totals(h, st);
