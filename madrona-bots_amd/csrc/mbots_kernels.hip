@@ -1446,14 +1446,16 @@ hipError_t launch_move(const SimState &S, const ObsTable &cur, const ObsTable &n
     if (parts & kMoveMain) {
         add(nxt.action, cur.action, 8, 3);
         add(nxt.hidden, cur.hidden, 16, 4);
+        add(nxt.psem, cur.sem, 16, 2);                   // prev sensor <- last step's sensor
+        if (S.flags & kFlagFixDepth) add(nxt.pdepth, cur.depth, 16, 2);
+    }
+    if (parts & kMovePrev6) {
         add(nxt.pspecies, lz ? cur.species : cur.pspecies, 4, 1);
         add(nxt.ppos, lz ? cur.pos : cur.ppos, 8, 1);
         add(nxt.phealth, lz ? cur.health : cur.phealth, 4, 1);
         add(nxt.psur, lz ? cur.sur : cur.psur, 8, 1);
         add(nxt.preward, lz ? cur.reward : cur.preward, 4, 1);
         add(nxt.pstats, lz ? cur.stats : cur.pstats, 16, 1, lz ? 1u : 0u);
-        add(nxt.psem, cur.sem, 16, 2);                   // prev sensor <- last step's sensor
-        if (S.flags & kFlagFixDepth) add(nxt.pdepth, cur.depth, 16, 2);
     }
     if (parts & kMovePrevAH) {
         add(nxt.paction, cur.paction, 8, 3);

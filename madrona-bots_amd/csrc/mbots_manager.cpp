@@ -75,8 +75,12 @@ struct mbots_handle {
     hipStream_t aux = nullptr;        // internal stream of the K3b sensor (forked after K2)
     hipEvent_t ev_join[2] = {nullptr, nullptr};   // K3b of alternate steps done (aux)
     int last_join = -1;               // ev_join of the latest K3b, -1: none pending
-    bool ah_pending[2] = {false, false};  // table half's PrevAction / PrevHiddenState not yet
-                                          // moved from the other half (deferred K4 part)
+    // deferred K4 parts of a table half (moved from the other half along the
+    // last src_of when needed): PrevAction / PrevHiddenState, the six other
+    // Prev* columns (from the other half's current ones when six_lazy)
+    bool ah_pending[2] = {false, false};
+    bool six_pending[2] = {false, false};
+    bool six_lazy[2] = {false, false};
     bool prev_lazy[2] = {false, false};   // table half's six shift-owned Prev* columns are
                                           // still its current ones (lazy shift, K5)
     uint64_t steps = 0;               // steps run
@@ -204,6 +208,13 @@ int wait_sensor(mbots_handle *h)
 // (on the stream the caller uses next)
 int materialize_prev(mbots_handle *h, hipStream_t st)
 {
+    if (h->six_pending[h->tb]) {   // a step's deferred move (no shift since)
+        HIP_TRY(hipSetDevice(h->device));
+        HIP_TRY(mbots::launch_move(h->S, h->T[h->tb ^ 1], h->T[h->tb], h->six_lazy[h->tb] ? 1 : 0,
+                                   mbots::kMovePrev6, st));
+        h->six_pending[h->tb] = false;
+        return MBOTS_OK;
+    }
     if (!h->prev_lazy[h->tb]) return MBOTS_OK;
     HIP_TRY(hipSetDevice(h->device));
     HIP_TRY(mbots::launch_shift(h->S, h->T[h->tb], mbots::kShiftRest, st));
@@ -413,6 +424,7 @@ int mbots_step(mbots_handle *h, void *stream)
     const int par = h->parity;
     const int lazy = h->prev_lazy[h->tb] ? 1 : 0;
     // no shift since the last step: its deferred Prev moves first
+    if (h->six_pending[h->tb] && (rc = materialize_prev(h, st))) return rc;
     if ((rc = materialize_prev_ah(h, st))) return rc;
     // K1 reads the finder slots the previous step's sensor wrote, and writes the
     // state half that sensor read; the halves swap after K1.
@@ -455,8 +467,11 @@ int mbots_step(mbots_handle *h, void *stream)
     ++h->steps;
     h->parity ^= 1;
     h->tb ^= 1;
-    h->prev_lazy[h->tb] = false;   // the move wrote every Prev* column of the new table
-    h->ah_pending[h->tb] = true;   // ... but PrevAction / PrevHiddenState (deferred)
+    // the new half's Prev* columns: eight moves deferred (a shift overwrites them)
+    h->prev_lazy[h->tb] = false;
+    h->ah_pending[h->tb] = true;
+    h->six_pending[h->tb] = true;
+    h->six_lazy[h->tb] = lazy != 0;
     return MBOTS_OK;
 }
 
@@ -475,6 +490,7 @@ int mbots_shift_observations(mbots_handle *h, void *stream)
     if (rc == MBOTS_OK) {
         h->prev_lazy[h->tb] = true;
         h->ah_pending[h->tb] = false;   // the shift wrote PrevAction / PrevHiddenState
+        h->six_pending[h->tb] = false;  // ... and made the six the current columns
     }
     return rc;
 }
@@ -603,6 +619,7 @@ int mbots_construct_obs(mbots_handle *h, int32_t prev, float *out, uint64_t out_
     h->last_stream = st;
     int rc;
     if (!prev && (rc = wait_sensor(h))) return rc;   // current semantic rows come from K3b
+    if (prev && h->six_pending[h->tb] && (rc = materialize_prev(h, st))) return rc;
     HIP_TRY(mbots::launch_construct_obs(h->S, h->T[h->tb], prev, h->prev_lazy[h->tb] ? 1 : 0, out,
                                         (uint32_t)out_rows, st));
     return MBOTS_OK;
@@ -711,6 +728,7 @@ int mbots_load_checkpoint(mbots_handle *h, const void *src, uint64_t bytes)
     h->last_join = -1;
     h->prev_lazy[0] = h->prev_lazy[1] = false;
     h->ah_pending[0] = h->ah_pending[1] = false;
+    h->six_pending[0] = h->six_pending[1] = false;
     h->steps = 1;
     hipStream_t st = nullptr;
     int rc = record_totals(h, st);
