@@ -369,9 +369,20 @@ int mbots_create(const mbots_config *cfg_in, mbots_handle **out)
             if ((i + 1) * k / ncu > i * k / ncu) mask[i / 32] |= 1u << (i % 32);
         check(hipExtStreamCreateWithCUMask(&h->aux, (uint32_t)mask.size(), mask.data()),
               "hipExtStreamCreateWithCUMask");
+    } else if (const char *e = getenv("MBOTS_AUX_PRIORITY")) {
+        check(hipStreamCreateWithPriority(&h->aux, hipStreamNonBlocking, atoi(e)),
+              "hipStreamCreateWithPriority");
     } else
 #endif
-    check(hipStreamCreateWithFlags(&h->aux, hipStreamNonBlocking), "hipStreamCreate");
+    {
+        // the sensor is the step's longer chain once the deferred Prev moves
+        // left the caller's stream lighter: its stream gets the higher priority
+        // (step -1.9 %, same box; DESIGN.md "Schedule")
+        int least = 0, greatest = 0;
+        check(hipDeviceGetStreamPriorityRange(&least, &greatest), "hipDeviceGetStreamPriorityRange");
+        check(hipStreamCreateWithPriority(&h->aux, hipStreamNonBlocking, greatest),
+              "hipStreamCreateWithPriority");
+    }
     hipStream_t st = nullptr;
     check(hipMemsetAsync(h->arena.base, 0, bytes, st), "hipMemsetAsync");
     // Sim::Sim / initWorld (sim.cpp:1232-1256) + initial export of the rows
