@@ -919,8 +919,9 @@ __device__ __forceinline__ void run_survivors(SensorLDS &L, int nf, int a0, int 
             // pixel coordinates s = (u + 1) sc - 0.5 (pixel k at s = k)
             const float sc = fwd ? 12.0f : 4.0f;
             const float sia = sc * __builtin_amdgcn_rcpf(f * f - 1.0f);
-            const float lo = (lf - sq) * sia + (fwd ? 12.0f * (1.0f - kUEps) - 0.5f : 4.0f * (1.0f - kUEps) - 0.5f);
-            const float hi = (lf + sq) * sia + (fwd ? 12.0f * (1.0f + kUEps) - 0.5f : 4.0f * (1.0f + kUEps) - 0.5f);
+            // (FMA: an approximation bounded by the kUEps margin either way)
+            const float lo = __builtin_fmaf(lf - sq, sia, fwd ? 12.0f * (1.0f - kUEps) - 0.5f : 4.0f * (1.0f - kUEps) - 0.5f);
+            const float hi = __builtin_fmaf(lf + sq, sia, fwd ? 12.0f * (1.0f + kUEps) - 0.5f : 4.0f * (1.0f + kUEps) - 0.5f);
             const int kmax = fwd ? 23 : 7;
             int k0 = max((int)ceilf(lo), 0);
             const int k1 = min((int)floorf(hi), kmax);
@@ -1106,7 +1107,9 @@ __global__ __launch_bounds__(64 * kSensorWorlds, MB_SENSOR_BLOCKS) void sensor_k
                 // branch-free: every lane reads a valid object and masks the result
                 const float2 p = L.obj[min(j, nobj - 1)];
                 const float vx = p.x - ap.x, vy = p.y - ap.y;
-                const float f = vx * ah.x + vy * ah.y, l = vx * ah.y - vy * ah.x;   // pair_fl
+                // pair_fl's (f, l) up to an FMA rounding: the cull's margin
+                // (kWedge - sqrt 2 = 0.05) dwarfs it; survivors recompute exactly
+                const float f = __builtin_fmaf(vx, ah.x, vy * ah.y), l = __builtin_fmaf(vx, ah.y, -(vy * ah.x));
                 const bool keep = (j < nobj) & (j != self) & (a < nc) & (fabsf(l) <= fabsf(f) + kWedge);
                 const uint64_t m = ballot64(keep);
                 if (keep) L.qcode[nq + (int)rank_below(m)] = (uint32_t)a | ((uint32_t)j << 11);
