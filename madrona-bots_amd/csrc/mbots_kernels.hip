@@ -62,7 +62,7 @@ constexpr int kWorldsPerBlock = 4;
 constexpr int kTileWorlds = 1024;             // worlds per scan tile (K2 block)
 
 #ifndef MB_NT
-#define MB_NT 35  // non-temporal stores: 1 K4, 2 K5, 4 K3a, 8 sensor output, 16 K4 but Action/Hidden;
+#define MB_NT 35  // non-temporal stores: 1 K4, 2 K5, 4 K3a, 8 sensor output;
                   // non-temporal loads: 32 K4 sources, 64 K5 sources
 #endif
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
@@ -751,6 +751,7 @@ __global__ __launch_bounds__(256) void export_rows_kernel(SimState S, ObsTable n
 // ---------------------------------------------------------------------------
 struct MoveSeg {
     void *dst;
+    void *dst2;       // a second destination (the fused shift's Prev column) or null
     const void *src;
     uint32_t width;   // bytes per item: 4, 8 or 16
     uint32_t ipr;     // items per row
@@ -769,19 +770,17 @@ __device__ __forceinline__ void move_item(const MoveSeg &sg, uint32_t idx, int32
     T v{};
     if (o >= 0) v = ld_stream(reinterpret_cast<const T *>(sg.src) + (size_t)o * sg.ipr + part, (MB_NT & 32) != 0);
     st_stream(reinterpret_cast<T *>(sg.dst) + idx, v, nt);
+    if (sg.dst2) st_stream(reinterpret_cast<T *>(sg.dst2) + idx, v, nt);
 }
 
-__global__ __launch_bounds__(256) void move_kernel(const uint32_t *totals, const int32_t *src_of,
-                                                   MoveArgs args, uint32_t tl_step)
+__device__ __forceinline__ void move_rows(const uint32_t *totals, const int32_t *src_of,
+                                          const MoveArgs &args)
 {
-    TL_SCOPE(4, tl_step);
     const uint32_t N = totals[0];
     const MoveSeg &sg = args.seg[blockIdx.y];
     const uint32_t items = N * sg.ipr;
     const uint32_t stride = gridDim.x * blockDim.x;
-    // (MB_NT & 16: segments 0, 1 -- Action / HiddenState, which the shift reads
-    // next -- keep plain stores)
-    const bool nt = (MB_NT & 1) || ((MB_NT & 16) && blockIdx.y >= 2);
+    const bool nt = (MB_NT & 1) != 0;
     for (uint32_t idx = blockIdx.x * blockDim.x + threadIdx.x; idx < items; idx += stride) {
         uint32_t r = idx, part = 0;
         if (sg.ipr == 2) { r = idx >> 1; part = idx & 1u; }
@@ -797,6 +796,22 @@ __global__ __launch_bounds__(256) void move_kernel(const uint32_t *totals, const
         else if (sg.width == 8) move_item<uint2>(sg, idx, o, part, nt);
         else move_item<uint32_t>(sg, idx, o, part, nt);
     }
+}
+
+__global__ __launch_bounds__(256) void move_kernel(const uint32_t *totals, const int32_t *src_of,
+                                                   MoveArgs args, uint32_t tl_step)
+{
+    TL_SCOPE(4, tl_step);
+    move_rows(totals, src_of, args);
+}
+
+// the fused shift (DESIGN.md "Deferred Prev moves"): Action / HiddenState
+// gathered from the other half into both the current and the Prev column
+__global__ __launch_bounds__(256) void shift_move_kernel(const uint32_t *totals, const int32_t *src_of,
+                                                         MoveArgs args, uint32_t tl_step)
+{
+    TL_SCOPE(5, tl_step);
+    move_rows(totals, src_of, args);
 }
 
 // ---------------------------------------------------------------------------
@@ -1441,14 +1456,18 @@ hipError_t launch_move(const SimState &S, const ObsTable &cur, const ObsTable &n
 {
     MoveArgs m{};
     int k = 0;
-    auto add = [&](void *d, const void *s, uint32_t width, uint32_t ipr, uint32_t xform = 0) {
-        m.seg[k++] = MoveSeg{d, s, width, ipr, xform};
+    auto add = [&](void *d, const void *s, uint32_t width, uint32_t ipr, uint32_t xform = 0,
+                   void *d2 = nullptr) {
+        m.seg[k++] = MoveSeg{d, d2, s, width, ipr, xform};
     };
     // after a lazy shift the six Prev* columns it left are the current ones
     const bool lz = prev_lazy != 0;
-    if (parts & kMoveMain) {
-        add(nxt.action, cur.action, 8, 3);
-        add(nxt.hidden, cur.hidden, 16, 4);
+    if (parts & (kMoveAH | kMoveAHShift)) {
+        const bool sh = (parts & kMoveAHShift) != 0;
+        add(nxt.action, cur.action, 8, 3, 0, sh ? nxt.paction : nullptr);
+        add(nxt.hidden, cur.hidden, 16, 4, 0, sh ? nxt.phidden : nullptr);
+    }
+    if (parts & kMoveSensor) {
         add(nxt.psem, cur.sem, 16, 2);                   // prev sensor <- last step's sensor
         if (S.flags & kFlagFixDepth) add(nxt.pdepth, cur.depth, 16, 2);
     }
@@ -1466,7 +1485,10 @@ hipError_t launch_move(const SimState &S, const ObsTable &cur, const ObsTable &n
     }
     if (k == 0) return hipSuccess;
     m.nseg = k;
-    hipLaunchKernelGGL(move_kernel, dim3(512, k), dim3(256), 0, st, S.totals, S.src_of, m, S.tl_step);
+    if (parts & kMoveAHShift)
+        hipLaunchKernelGGL(shift_move_kernel, dim3(512, k), dim3(256), 0, st, S.totals, S.src_of, m, S.tl_step);
+    else
+        hipLaunchKernelGGL(move_kernel, dim3(512, k), dim3(256), 0, st, S.totals, S.src_of, m, S.tl_step);
     return hipGetLastError();
 }
 hipError_t launch_sensor(const SimState &S, const ObsTable &nxt, hipStream_t st)

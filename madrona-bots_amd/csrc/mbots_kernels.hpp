@@ -64,10 +64,11 @@ hipError_t launch_tile_sum(const SimState &S, int parity, hipStream_t st);
 hipError_t launch_world_step(const SimState &S, const ObsTable &cur, int parity, hipStream_t st);
 hipError_t launch_scan(const SimState &S, int parity, hipStream_t st);
 hipError_t launch_export_rows(const SimState &S, const ObsTable &nxt, int init, hipStream_t st);
-// K4 parts: Action, HiddenState and the prev sensor; PrevAction /
-// PrevHiddenState; the six other Prev* columns (the last two deferred: a shift
-// overwrites them, DESIGN.md "Deferred Prev moves")
-constexpr int kMoveMain = 1, kMovePrevAH = 2, kMovePrev6 = 4, kMoveAll = 7;
+// K4 parts (DESIGN.md "Deferred Prev moves"): Action + HiddenState; the same
+// also into PrevAction / PrevHiddenState (the fused shift); the prev sensor;
+// PrevAction / PrevHiddenState; the six other Prev* columns
+constexpr int kMoveAH = 1, kMoveAHShift = 2, kMoveSensor = 4, kMovePrevAH = 8, kMovePrev6 = 16;
+constexpr int kMoveAll = kMoveAH | kMoveSensor | kMovePrevAH | kMovePrev6;
 hipError_t launch_move(const SimState &S, const ObsTable &cur, const ObsTable &nxt, int prev_lazy,
                        int parts, hipStream_t st);
 hipError_t launch_sensor(const SimState &S, const ObsTable &nxt, hipStream_t st);

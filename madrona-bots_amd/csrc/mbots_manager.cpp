@@ -78,6 +78,7 @@ struct mbots_handle {
     // deferred K4 parts of a table half (moved from the other half along the
     // last src_of when needed): PrevAction / PrevHiddenState, the six other
     // Prev* columns (from the other half's current ones when six_lazy)
+    bool cur_ah_pending[2] = {false, false};   // Action / HiddenState themselves
     bool ah_pending[2] = {false, false};
     bool six_pending[2] = {false, false};
     bool six_lazy[2] = {false, false};
@@ -231,6 +232,17 @@ int materialize_prev_ah(mbots_handle *h, hipStream_t st)
     HIP_TRY(hipSetDevice(h->device));
     HIP_TRY(mbots::launch_move(h->S, h->T[h->tb ^ 1], h->T[h->tb], 0, mbots::kMovePrevAH, st));
     h->ah_pending[h->tb] = false;
+    return MBOTS_OK;
+}
+
+// the deferred Action / HiddenState move of the current half (K1, the learner
+// and every accessor of the two columns need it; a shift fuses it)
+int materialize_cur_ah(mbots_handle *h, hipStream_t st)
+{
+    if (!h->cur_ah_pending[h->tb]) return MBOTS_OK;
+    HIP_TRY(hipSetDevice(h->device));
+    HIP_TRY(mbots::launch_move(h->S, h->T[h->tb ^ 1], h->T[h->tb], 0, mbots::kMoveAH, st));
+    h->cur_ah_pending[h->tb] = false;
     return MBOTS_OK;
 }
 
@@ -437,6 +449,7 @@ int mbots_step(mbots_handle *h, void *stream)
     // no shift since the last step: its deferred Prev moves first
     if (h->six_pending[h->tb] && (rc = materialize_prev(h, st))) return rc;
     if ((rc = materialize_prev_ah(h, st))) return rc;
+    if ((rc = materialize_cur_ah(h, st))) return rc;
     // K1 reads the finder slots the previous step's sensor wrote, and writes the
     // state half that sensor read; the halves swap after K1.
     if (h->last_join >= 0) HIP_TRY(hipStreamWaitEvent(st, h->ev_join[h->last_join], 0));
@@ -452,7 +465,7 @@ int mbots_step(mbots_handle *h, void *stream)
                     [&] { return mbots::launch_export_rows(h->S, nxt, 0, st); })))
         return rc;
     if ((rc = timed(h, MBOTS_TK_MOVE, st,
-                    [&] { return mbots::launch_move(h->S, cur, nxt, lazy, mbots::kMoveMain, st); })))
+                    [&] { return mbots::launch_move(h->S, cur, nxt, lazy, mbots::kMoveSensor, st); })))
         return rc;
     if ((rc = timed(h, MBOTS_TK_SENSOR, st, [&] { return mbots::launch_sensor(h->S, nxt, st); })))
         return rc;
@@ -472,7 +485,7 @@ int mbots_step(mbots_handle *h, void *stream)
                     [&] { return mbots::launch_export_rows(h->S, nxt, 0, st); })))
         return rc;
     if ((rc = timed(h, MBOTS_TK_MOVE, st,
-                    [&] { return mbots::launch_move(h->S, cur, nxt, lazy, mbots::kMoveMain, st); })))
+                    [&] { return mbots::launch_move(h->S, cur, nxt, lazy, mbots::kMoveSensor, st); })))
         return rc;
 #endif
     ++h->steps;
@@ -480,6 +493,7 @@ int mbots_step(mbots_handle *h, void *stream)
     h->tb ^= 1;
     // the new half's Prev* columns: eight moves deferred (a shift overwrites them)
     h->prev_lazy[h->tb] = false;
+    h->cur_ah_pending[h->tb] = true;
     h->ah_pending[h->tb] = true;
     h->six_pending[h->tb] = true;
     h->six_lazy[h->tb] = lazy != 0;
@@ -495,10 +509,15 @@ int mbots_shift_observations(mbots_handle *h, void *stream)
     // Action / HiddenState now (the learner overwrites them next); the other six
     // Prev* columns stay views of the current ones until the next step or an
     // accessor needs them (K5, lazy shift)
+    // (Action / HiddenState still in the other half: one gather writes them and
+    // their Prev copies -- the fused shift)
+    const bool fused = h->cur_ah_pending[h->tb];
     const int rc = timed(h, MBOTS_TK_SHIFT, st, [&] {
-        return mbots::launch_shift(h->S, h->T[h->tb], mbots::kShiftEager, st);
+        return fused ? mbots::launch_move(h->S, h->T[h->tb ^ 1], h->T[h->tb], 0, mbots::kMoveAHShift, st)
+                     : mbots::launch_shift(h->S, h->T[h->tb], mbots::kShiftEager, st);
     });
     if (rc == MBOTS_OK) {
+        h->cur_ah_pending[h->tb] = false;
         h->prev_lazy[h->tb] = true;
         h->ah_pending[h->tb] = false;   // the shift wrote PrevAction / PrevHiddenState
         h->six_pending[h->tb] = false;  // ... and made the six the current columns
@@ -529,6 +548,9 @@ int mbots_export(mbots_handle *h, int32_t id, mbots_tensor *out)
         break;
     case MBOTS_EXPORT_PREV_ACTION: case MBOTS_EXPORT_PREV_HIDDEN_STATE:
         if ((rc = materialize_prev_ah(h, h->last_stream))) return rc;
+        break;
+    case MBOTS_EXPORT_ACTION: case MBOTS_EXPORT_HIDDEN_STATE:
+        if ((rc = materialize_cur_ah(h, h->last_stream))) return rc;
         break;
     default: break;
     }
@@ -592,6 +614,7 @@ int mbots_set_action(mbots_handle *h, uint32_t row, const int32_t action[6])
     int rc = mbots_num_agents(h, &N);
     if (rc) return rc;
     if (row >= N) return fail(MBOTS_E_RANGE, "agent row out of range");
+    if ((rc = materialize_cur_ah(h, h->last_stream))) return rc;
     HIP_TRY(hipMemcpyAsync(h->T[h->tb].action + (size_t)row * 6, action, 6 * sizeof(int32_t),
                            hipMemcpyHostToDevice, h->last_stream));
     HIP_TRY(hipStreamSynchronize(h->last_stream));
@@ -616,6 +639,9 @@ int mbots_write_synthetic_actions(mbots_handle *h, uint32_t seed, uint32_t step,
     if (!h) return fail(MBOTS_E_INVALID, "null handle");
     HIP_TRY(hipSetDevice(h->device));
     hipStream_t st = as_stream(stream);
+    h->last_stream = st;
+    int rc = materialize_cur_ah(h, st);
+    if (rc) return rc;
     return timed(h, MBOTS_TK_ACTIONS, st, [&] {
         return mbots::launch_synthetic_actions(h->S, h->T[h->tb], seed, step, write_hidden, st);
     });
@@ -680,6 +706,7 @@ int mbots_save_checkpoint(mbots_handle *h, void *dst, uint64_t bytes)
     HIP_TRY(hipSetDevice(h->device));
     int rc0 = materialize_prev(h, h->last_stream);
     if (!rc0) rc0 = materialize_prev_ah(h, h->last_stream);
+    if (!rc0) rc0 = materialize_cur_ah(h, h->last_stream);
     if (rc0) return rc0;
     HIP_TRY(hipDeviceSynchronize());   // the sensor's finder / semantic rows included
     int rc = sync_totals(h);
@@ -740,6 +767,7 @@ int mbots_load_checkpoint(mbots_handle *h, const void *src, uint64_t bytes)
     h->prev_lazy[0] = h->prev_lazy[1] = false;
     h->ah_pending[0] = h->ah_pending[1] = false;
     h->six_pending[0] = h->six_pending[1] = false;
+    h->cur_ah_pending[0] = h->cur_ah_pending[1] = false;
     h->steps = 1;
     hipStream_t st = nullptr;
     int rc = record_totals(h, st);
