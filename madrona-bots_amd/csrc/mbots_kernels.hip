@@ -257,9 +257,9 @@ __device__ void world_step(SimState &S, const ObsTable &cur, WorldLDS &L, uint32
     uint32_t ctr = S.ctr[w];
     int32_t cur_food = S.cur_food[w];
     {
-        // slots < 64: loaded without waiting for n0 (slots past n0 are stale
-        // and dropped), so only the action rows wait on a second round trip
-        const bool in = lane < cap;
+        // slots < min(n0, 64) (n0 is one scalar load; the first wave round is
+        // bandwidth-bound, so the ~half of the lanes past n0 stay idle: K1 -2.4 %)
+        const bool in = (int)lane < n0;
         const size_t i = base + lane;
         const int32_t row = in ? S.obsrow[i] : -1;
         const float x = in ? S.x[i] : 0.0f, y = in ? S.y[i] : 0.0f;
