@@ -298,7 +298,7 @@ def main():
         nb = algorithmic_bytes(mean_agents, W)
         achieved = nb / (span_ms * 1e-3) / 1e9
         roof = {"bound": "hbm", "kernel": "world step: step()+shift_observations() "
-                "(K1 world_step, K2 scan, K3a export_rows, K4 move || K3b sensor, K5 shift)",
+                "(K1 world_step, K2 scan, K3a export_rows, K4 move, K5 shift (fused gather) || K3b sensor)",
                 "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                 "algorithmic_bytes_per_launch": nb, "avg_launch_ms": span_ms,
@@ -323,6 +323,9 @@ def main():
             if tr:
                 kst, kst_src = load_kernel_stats()
                 kh = {}
+                # a shift that follows a step is the fused gather (shift_move_kernel)
+                if "shift_move_kernel" in tr[1]["kernels"]:
+                    kmap["shift"] = "shift_move_kernel"
                 for k, kn in kmap.items():
                     b = tr[1]["kernels"].get(kn, {}).get("hbm_bytes_per_launch")
                     if b and per.get(k):

@@ -30,7 +30,7 @@ for (cn, k), byd in vals.items():
     ds = sorted(byd)[-5:]                      # last launches (steady state)
     per.setdefault(k, {})[cn] = sum(byd[d] for d in ds) / len(ds)
 step_kernels = ("world_step_kernel", "scan_kernel", "export_rows_kernel", "move_kernel",
-                "sensor_kernel", "shift_kernel")
+                "sensor_kernel", "shift_kernel", "shift_move_kernel")
 res = {"worlds": worlds, "correction": "bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024",
        "kernels": {}}
 tot = 0.0
