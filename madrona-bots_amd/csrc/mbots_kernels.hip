@@ -13,6 +13,7 @@
 // (current observations, reward, old->new row map) -> K4 move (Action, Hidden,
 // Prev*, prev sensor to the new rows).  shift_observations() = K5 shift.
 // DESIGN.md section 4 has the schedule and each kernel's bound.
+#include <hip/hip_ext.h>
 #include "mbots_kernels.hpp"
 #include <stdlib.h>
 #include "mbots_ray.hpp"
@@ -1441,9 +1442,11 @@ hipError_t launch_world_step(const SimState &S, const ObsTable &cur, int parity,
     hipLaunchKernelGGL(world_step_kernel, dim3(world_blocks(S.W)), dim3(256), 0, st, S, cur, parity);
     return hipGetLastError();
 }
-hipError_t launch_scan(const SimState &S, int parity, hipStream_t st)
+hipError_t launch_scan(const SimState &S, int parity, hipStream_t st, hipEvent_t done)
 {
-    hipLaunchKernelGGL(scan_kernel, dim3(S.ntiles), dim3(1024), 0, st, S, parity);
+    // `done` rides on the dispatch packet itself (no marker packet between K2
+    // and the next kernel on this stream)
+    hipExtLaunchKernelGGL(scan_kernel, dim3(S.ntiles), dim3(1024), 0, st, nullptr, done, 0u, S, parity);
     return hipGetLastError();
 }
 hipError_t launch_export_rows(const SimState &S, const ObsTable &nxt, int init, hipStream_t st)
@@ -1491,7 +1494,7 @@ hipError_t launch_move(const SimState &S, const ObsTable &cur, const ObsTable &n
         hipLaunchKernelGGL(move_kernel, dim3(512, k), dim3(256), 0, st, S.totals, S.src_of, m, S.tl_step);
     return hipGetLastError();
 }
-hipError_t launch_sensor(const SimState &S, const ObsTable &nxt, hipStream_t st)
+hipError_t launch_sensor(const SimState &S, const ObsTable &nxt, hipStream_t st, hipEvent_t done)
 {
     size_t pad = 0;
 #ifdef MB_KNOBS
@@ -1503,12 +1506,12 @@ hipError_t launch_sensor(const SimState &S, const ObsTable &nxt, hipStream_t st)
     if (S.W <= (uint32_t)MB_SENSOR_SPLIT_MAX) {   // small: MB_SENSOR_SPLIT waves per world
         constexpr int kWpb = kSensorWorlds / MB_SENSOR_SPLIT;
         const dim3 grid((S.W + kWpb - 1) / kWpb);
-        if (fixd) hipLaunchKernelGGL((sensor_kernel<true, MB_SENSOR_SPLIT>), grid, blk, pad, st, S, nxt);
-        else hipLaunchKernelGGL((sensor_kernel<false, MB_SENSOR_SPLIT>), grid, blk, pad, st, S, nxt);
+        if (fixd) hipExtLaunchKernelGGL((sensor_kernel<true, MB_SENSOR_SPLIT>), grid, blk, (uint32_t)pad, st, nullptr, done, 0u, S, nxt);
+        else hipExtLaunchKernelGGL((sensor_kernel<false, MB_SENSOR_SPLIT>), grid, blk, (uint32_t)pad, st, nullptr, done, 0u, S, nxt);
     } else {
         const dim3 grid((S.W + kSensorWorlds - 1) / kSensorWorlds);
-        if (fixd) hipLaunchKernelGGL((sensor_kernel<true, 1>), grid, blk, pad, st, S, nxt);
-        else hipLaunchKernelGGL((sensor_kernel<false, 1>), grid, blk, pad, st, S, nxt);
+        if (fixd) hipExtLaunchKernelGGL((sensor_kernel<true, 1>), grid, blk, (uint32_t)pad, st, nullptr, done, 0u, S, nxt);
+        else hipExtLaunchKernelGGL((sensor_kernel<false, 1>), grid, blk, (uint32_t)pad, st, nullptr, done, 0u, S, nxt);
     }
     return hipGetLastError();
 }

@@ -367,9 +367,10 @@ int mbots_create(const mbots_config *cfg_in, mbots_handle **out)
     if (rc == MBOTS_OK)
         check(hipHostGetDevicePointer((void **)&S.totals_host, h->h_totals, 0),
               "hipHostGetDevicePointer");
-    check(hipEventCreateWithFlags(&h->ev_totals, hipEventDisableTiming), "hipEventCreate");
-    check(hipEventCreateWithFlags(&h->ev_join[0], hipEventDisableTiming), "hipEventCreate");
-    check(hipEventCreateWithFlags(&h->ev_join[1], hipEventDisableTiming), "hipEventCreate");
+    // (default flags: these ride on kernel dispatches as their stop events)
+    check(hipEventCreate(&h->ev_totals), "hipEventCreate");
+    check(hipEventCreate(&h->ev_join[0]), "hipEventCreate");
+    check(hipEventCreate(&h->ev_join[1]), "hipEventCreate");
 #ifdef MB_KNOBS
     // occupancy experiment: the sensor stream on a CU subset spread evenly
     if (const char *e = getenv("MBOTS_SENSOR_CUS")) {
@@ -457,9 +458,10 @@ int mbots_step(mbots_handle *h, void *stream)
                     [&] { return mbots::launch_world_step(h->S, cur, par, st); })))
         return rc;
     mbots::swap_state(h->S);
-    if ((rc = timed(h, MBOTS_TK_SCAN, st, [&] { return mbots::launch_scan(h->S, par, st); }))) return rc;
-    // K2 wrote the row counts into the pinned mirror; accessors wait on this
-    HIP_TRY(hipEventRecord(h->ev_totals, st));
+    // K2 writes the row counts into the pinned mirror; accessors and the
+    // sensor's stream wait on ev_totals, carried by K2's own dispatch
+    if ((rc = timed(h, MBOTS_TK_SCAN, st, [&] { return mbots::launch_scan(h->S, par, st, h->ev_totals); })))
+        return rc;
 #ifdef MB_NO_FORK
     if ((rc = timed(h, MBOTS_TK_EXPORT, st,
                     [&] { return mbots::launch_export_rows(h->S, nxt, 0, st); })))
@@ -477,9 +479,9 @@ int mbots_step(mbots_handle *h, void *stream)
     // next step's K1 and the semantic/depth accessors wait for ev_join.
     const int jcur = h->last_join == 0 ? 1 : 0;
     HIP_TRY(hipStreamWaitEvent(h->aux, h->ev_totals, 0));
-    if ((rc = timed(h, MBOTS_TK_SENSOR, h->aux, [&] { return mbots::launch_sensor(h->S, nxt, h->aux); })))
+    if ((rc = timed(h, MBOTS_TK_SENSOR, h->aux,
+                    [&] { return mbots::launch_sensor(h->S, nxt, h->aux, h->ev_join[jcur]); })))
         return rc;
-    HIP_TRY(hipEventRecord(h->ev_join[jcur], h->aux));
     h->last_join = jcur;
     if ((rc = timed(h, MBOTS_TK_EXPORT, st,
                     [&] { return mbots::launch_export_rows(h->S, nxt, 0, st); })))
