@@ -857,7 +857,8 @@ struct SensorLDS {
     float2 hd[kMaxCap];                       // agent headings
     int8_t sp[kMaxCap];
     alignas(16) uint32_t key[kKeyAgents * kKeyStride];
-    uint32_t qcode[kQueueCap];                // P1 survivors: agent | object << 11
+    uint32_t qcode[kQueueCap + 1];            // P1 survivors: agent | object << 11 (+ a
+                                              // sink slot for the branch-free write)
     uint32_t wcode[kWideCap];                 // wide pairs: code, f, l
     float wf[kWideCap], wl[kWideCap];
     alignas(16) float u[kSensor];
@@ -1128,7 +1129,8 @@ __global__ __launch_bounds__(64 * kSensorWorlds, MB_SENSOR_BLOCKS) void sensor_k
                 const float f = __builtin_fmaf(vx, ah.x, vy * ah.y), l = __builtin_fmaf(vx, ah.y, -(vy * ah.x));
                 const bool keep = (j < nobj) & (j != self) & (a < nc) & (fabsf(l) <= fabsf(f) + kWedge);
                 const uint64_t m = ballot64(keep);
-                if (keep) L.qcode[nq + (int)rank_below(m)] = (uint32_t)a | ((uint32_t)j << 11);
+                // branch-free: culled lanes write the sink slot (+1 % step)
+                L.qcode[keep ? nq + (int)rank_below(m) : kQueueCap] = (uint32_t)a | ((uint32_t)j << 11);
                 nq += __popcll(m);
                 if (nq >= 64) {
                     wave_sync();
