@@ -85,3 +85,44 @@ def test_world_state_matches_oracle():
         assert np.array_equal(g["health"], o["health"])
         assert np.array_equal(g["finder"], o["finder"])
         assert g["food"].shape[1] == 3 and len(g["food"]) <= 30
+
+
+@pytest.mark.gpu
+def test_checkpoint_between_step_and_shift(tmp_path):
+    """A save right after step() (every deferred Prev move and the Action /
+    HiddenState move still pending) restores to the same state: both managers
+    then shift and step on identically."""
+    import madrona_bots as mb
+    a = mb.SimManager(0, 48, 5, 24)
+    _run(a, 0, 4)
+    a.write_synthetic_actions(1234, 4, write_hidden=True)
+    a.step()                                 # no accessor, no shift
+    path = str(tmp_path / "mid.bin")
+    a.save_checkpoint(path)
+    b = mb.SimManager(0, 48, 5, 24)
+    b.load_checkpoint(path)
+    for sim in (a, b):
+        sim.shift_observations()
+        _run(sim, 5, 8)
+    ra, rb = _snap(a), _snap(b)
+    for k in ra:
+        assert torch.equal(ra[k], rb[k]), k
+
+
+@pytest.mark.gpu
+def test_set_action_after_step_then_shift():
+    """set_action between step() and shift_observations() lands in the row the
+    shift copies to PrevAction (the deferred Action move runs first)."""
+    import madrona_bots as mb
+    m = mb.SimManager(0, 16, 69, 32)
+    m.write_synthetic_actions(1234, 0)
+    m.step()
+    before = m.action_tensor(False).to_torch().clone()
+    m.step()
+    m.set_action(3, 1, 0, 1, 0, 1, 0)
+    m.shift_observations()
+    prev = m.action_tensor(True).to_torch()
+    cur = m.action_tensor(False).to_torch()
+    assert prev[3].tolist() == [1, 0, 1, 0, 1, 0]
+    assert torch.equal(prev, cur)
+    assert before.shape[1] == 6
