@@ -749,6 +749,11 @@ __global__ __launch_bounds__(256) void export_rows_kernel(SimState S, ObsTable n
 // stream of 8/16-byte items over the new rows, so stores are fully coalesced
 // and the gathered loads are contiguous wherever old rows are (most agents
 // keep their species and relative order).
+//
+// A step launches only the prev-sensor part; the other parts are deferred
+// (DESIGN.md "Deferred Prev moves") and run from the host's materialisation
+// points, or fused with the shift (shift_move_kernel: Action / HiddenState into
+// both the current and the Prev column).
 // ---------------------------------------------------------------------------
 struct MoveSeg {
     void *dst;
@@ -1303,6 +1308,8 @@ __global__ __launch_bounds__(256) void construct_obs_kernel(const uint32_t *tota
 // Reward, Stats} as a view of the current columns: the next step moves them
 // from there, construct_obs reads them there, and an accessor of one of them
 // materialises the copy first (kShiftRest).  kShiftAll copies all eight.
+// A shift right after a step runs shift_move_kernel instead (the deferred
+// Action / HiddenState move fused with this copy).
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void shift_kernel(const uint32_t *totals, ObsTable t, int mode,
                                                     uint32_t tl_step)
