@@ -588,15 +588,17 @@ __global__ __launch_bounds__(1024) void scan_kernel(SimState S, int parity)
     const int t = threadIdx.x, b = blockIdx.x;
     const int wv = t >> 6, lane = t & 63;
     const int32_t *tiles = S.tiles + (size_t)parity * S.ntiles * 5;
-    if (t < 5) {
+    // wave k < 5 sums counter k over the tiles, 64 tiles per pass
+    if (wv < 5) {
         int32_t pre = 0, tot = 0;
-        for (uint32_t tt = 0; tt < S.ntiles; ++tt) {
-            const int32_t v = tiles[tt * 5 + t];
+        for (uint32_t tt = lane; tt < S.ntiles; tt += 64) {
+            const int32_t v = tiles[tt * 5 + wv];
             if ((int)tt < b) pre += v;
             tot += v;
         }
-        s_pre[t] = pre;
-        s_tot[t] = tot;
+        pre = wave_incl_scan(pre);
+        tot = wave_incl_scan(tot);
+        if (lane == 63) { s_pre[wv] = pre; s_tot[wv] = tot; }
     }
     const uint32_t w = (uint32_t)b * kTileWorlds + (uint32_t)t;
     int32_t c[5] = {0, 0, 0, 0, 0};
@@ -642,7 +644,7 @@ __global__ __launch_bounds__(1024) void scan_kernel(SimState S, int parity)
             for (int k = 0; k < 5; ++k)
                 __hip_atomic_store(S.totals_host + k, k ? (uint32_t)s_tot[k - 1] : (uint32_t)s_tot[4],
                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            __threadfence_system();
+            // (the dispatch's completion signal releases at system scope)
         }
     }
 }
