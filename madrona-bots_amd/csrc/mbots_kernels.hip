@@ -1503,8 +1503,9 @@ hipError_t launch_move(const SimState &S, const ObsTable &cur, const ObsTable &n
 #define MB_MOVE_BLOCKS 8192   // +0.9 % vs 512 (4096: +0.6 %, 1024/2048 slower)
 #endif
     // blocks per segment: a launch of few segments (the prev sensor alone, the
-    // fused shift's two) still needs enough waves in flight to stream
-    const unsigned bx = k <= 2 ? (unsigned)MB_MOVE_BLOCKS : 512u;
+    // fused shift with or without the prev sensor) still needs enough waves in
+    // flight to stream
+    const unsigned bx = k <= 4 ? (unsigned)MB_MOVE_BLOCKS : 512u;
     if (parts & kMoveAHShift)
         hipLaunchKernelGGL(shift_move_kernel, dim3(bx, k), dim3(256), 0, st, S.totals, S.src_of, m, S.tl_step);
     else

@@ -79,6 +79,7 @@ struct mbots_handle {
     // last src_of when needed): PrevAction / PrevHiddenState, the six other
     // Prev* columns (from the other half's current ones when six_lazy)
     bool cur_ah_pending[2] = {false, false};   // Action / HiddenState themselves
+    bool psem_pending[2] = {false, false};     // the prev sensor (fused into the shift)
     bool ah_pending[2] = {false, false};
     bool six_pending[2] = {false, false};
     bool six_lazy[2] = {false, false};
@@ -243,6 +244,17 @@ int materialize_cur_ah(mbots_handle *h, hipStream_t st)
     HIP_TRY(hipSetDevice(h->device));
     HIP_TRY(mbots::launch_move(h->S, h->T[h->tb ^ 1], h->T[h->tb], 0, mbots::kMoveAH, st));
     h->cur_ah_pending[h->tb] = false;
+    return MBOTS_OK;
+}
+
+// the deferred prev-sensor move of the current half (accessors of the prev
+// sensor, construct_obs(prev), checkpoints, the next step; a shift fuses it)
+int materialize_psem(mbots_handle *h, hipStream_t st)
+{
+    if (!h->psem_pending[h->tb]) return MBOTS_OK;
+    HIP_TRY(hipSetDevice(h->device));
+    HIP_TRY(mbots::launch_move(h->S, h->T[h->tb ^ 1], h->T[h->tb], 0, mbots::kMoveSensor, st));
+    h->psem_pending[h->tb] = false;
     return MBOTS_OK;
 }
 
@@ -451,6 +463,7 @@ int mbots_step(mbots_handle *h, void *stream)
     if (h->six_pending[h->tb] && (rc = materialize_prev(h, st))) return rc;
     if ((rc = materialize_prev_ah(h, st))) return rc;
     if ((rc = materialize_cur_ah(h, st))) return rc;
+    if ((rc = materialize_psem(h, st))) return rc;   // before this step's sensor rewrites its source
     // K1 reads the finder slots the previous step's sensor wrote, and writes the
     // state half that sensor read; the halves swap after K1.
     if (h->last_join >= 0) HIP_TRY(hipStreamWaitEvent(st, h->ev_join[h->last_join], 0));
@@ -486,9 +499,6 @@ int mbots_step(mbots_handle *h, void *stream)
     if ((rc = timed(h, MBOTS_TK_EXPORT, st,
                     [&] { return mbots::launch_export_rows(h->S, nxt, 0, st); })))
         return rc;
-    if ((rc = timed(h, MBOTS_TK_MOVE, st,
-                    [&] { return mbots::launch_move(h->S, cur, nxt, lazy, mbots::kMoveSensor, st); })))
-        return rc;
 #endif
     ++h->steps;
     h->parity ^= 1;
@@ -496,6 +506,9 @@ int mbots_step(mbots_handle *h, void *stream)
     // the new half's Prev* columns: eight moves deferred (a shift overwrites them)
     h->prev_lazy[h->tb] = false;
     h->cur_ah_pending[h->tb] = true;
+#ifndef MB_NO_FORK
+    h->psem_pending[h->tb] = true;
+#endif
     h->ah_pending[h->tb] = true;
     h->six_pending[h->tb] = true;
     h->six_lazy[h->tb] = lazy != 0;
@@ -513,13 +526,17 @@ int mbots_shift_observations(mbots_handle *h, void *stream)
     // accessor needs them (K5, lazy shift)
     // (Action / HiddenState still in the other half: one gather writes them and
     // their Prev copies -- the fused shift)
+    // (and the prev sensor rides along when still pending)
     const bool fused = h->cur_ah_pending[h->tb];
+    const bool with_psem = fused && h->psem_pending[h->tb];
     const int rc = timed(h, MBOTS_TK_SHIFT, st, [&] {
-        return fused ? mbots::launch_move(h->S, h->T[h->tb ^ 1], h->T[h->tb], 0, mbots::kMoveAHShift, st)
+        return fused ? mbots::launch_move(h->S, h->T[h->tb ^ 1], h->T[h->tb], 0,
+                                          mbots::kMoveAHShift | (with_psem ? mbots::kMoveSensor : 0), st)
                      : mbots::launch_shift(h->S, h->T[h->tb], mbots::kShiftEager, st);
     });
     if (rc == MBOTS_OK) {
         h->cur_ah_pending[h->tb] = false;
+        if (with_psem) h->psem_pending[h->tb] = false;
         h->prev_lazy[h->tb] = true;
         h->ah_pending[h->tb] = false;   // the shift wrote PrevAction / PrevHiddenState
         h->six_pending[h->tb] = false;  // ... and made the six the current columns
@@ -553,6 +570,9 @@ int mbots_export(mbots_handle *h, int32_t id, mbots_tensor *out)
         break;
     case MBOTS_EXPORT_ACTION: case MBOTS_EXPORT_HIDDEN_STATE:
         if ((rc = materialize_cur_ah(h, h->last_stream))) return rc;
+        break;
+    case MBOTS_EXPORT_PREV_SENSOR_SEMANTIC: case MBOTS_EXPORT_PREV_SENSOR_DEPTH:
+        if ((rc = materialize_psem(h, h->last_stream))) return rc;
         break;
     default: break;
     }
@@ -659,6 +679,7 @@ int mbots_construct_obs(mbots_handle *h, int32_t prev, float *out, uint64_t out_
     int rc;
     if (!prev && (rc = wait_sensor(h))) return rc;   // current semantic rows come from K3b
     if (prev && h->six_pending[h->tb] && (rc = materialize_prev(h, st))) return rc;
+    if (prev && (rc = materialize_psem(h, st))) return rc;
     HIP_TRY(mbots::launch_construct_obs(h->S, h->T[h->tb], prev, h->prev_lazy[h->tb] ? 1 : 0, out,
                                         (uint32_t)out_rows, st));
     return MBOTS_OK;
@@ -709,6 +730,7 @@ int mbots_save_checkpoint(mbots_handle *h, void *dst, uint64_t bytes)
     int rc0 = materialize_prev(h, h->last_stream);
     if (!rc0) rc0 = materialize_prev_ah(h, h->last_stream);
     if (!rc0) rc0 = materialize_cur_ah(h, h->last_stream);
+    if (!rc0) rc0 = materialize_psem(h, h->last_stream);
     if (rc0) return rc0;
     HIP_TRY(hipDeviceSynchronize());   // the sensor's finder / semantic rows included
     int rc = sync_totals(h);
@@ -770,6 +792,7 @@ int mbots_load_checkpoint(mbots_handle *h, const void *src, uint64_t bytes)
     h->ah_pending[0] = h->ah_pending[1] = false;
     h->six_pending[0] = h->six_pending[1] = false;
     h->cur_ah_pending[0] = h->cur_ah_pending[1] = false;
+    h->psem_pending[0] = h->psem_pending[1] = false;
     h->steps = 1;
     hipStream_t st = nullptr;
     int rc = record_totals(h, st);
