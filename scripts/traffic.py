@@ -34,12 +34,17 @@ step_kernels = ("world_step_kernel", "scan_kernel", "export_rows_kernel", "move_
 res = {"worlds": worlds, "correction": "bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024",
        "kernels": {}}
 tot = 0.0
+# launches per step: a kernel a step does not launch every time (move_kernel
+# runs at init and on deferred-move materialisation only) counts by its share
+launches = {k: len(byd) for (cn, k), byd in vals.items() if cn == "FETCH_SIZE"}
+n_steps = max(launches.get("world_step_kernel", 1), 1)
 for k, c in sorted(per.items()):
     b = (2.0 * c.get("FETCH_SIZE", 0.0) + c.get("WRITE_SIZE", 0.0)) * 1024.0
+    share = min(launches.get(k, n_steps) / n_steps, 1.0)
     res["kernels"][k] = {"FETCH_SIZE_KB": c.get("FETCH_SIZE"), "WRITE_SIZE_KB": c.get("WRITE_SIZE"),
-                         "hbm_bytes_per_launch": b}
+                         "hbm_bytes_per_launch": b, "launches_per_step": share}
     if k in step_kernels:
-        tot += b
+        tot += b * share
 res["bytes_per_step"] = tot
 json.dump(res, open(out, "w"), indent=1)
 print(json.dumps(res, indent=1))
