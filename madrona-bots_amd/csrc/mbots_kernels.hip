@@ -20,45 +20,6 @@
 
 namespace mbots {
 
-#ifdef MB_PROF
-// per-phase shader-clock accounting (instrumentation builds only)
-// 64 slots per counter (by block) keep the accounting atomics uncontended
-__device__ unsigned long long g_sprof[64 * 8];
-__device__ unsigned long long g_kprof[64 * 8];
-#define PROF_NOW() __builtin_amdgcn_s_memtime()
-#define PROF_ADD(k, v) (prof[k] += (v))
-#else
-#define PROF_NOW() 0ull
-#define PROF_ADD(k, v) ((void)0)
-#endif
-
-#ifdef MB_TL
-// kernel timeline (instrumentation builds only): per launch of each kernel the
-// earliest wave start and latest wave end on the 100 MHz realtime clock, so a
-// step's schedule (gaps, overlap) is seen without a profiler in the process.
-// launch index = wave ticket / waves per launch (launches of one kernel never
-// overlap: each kernel has a single stream).
-constexpr int kTlKernels = 8, kTlSlots = 64, kTlSpread = 64;
-// [slot][kernel][spread][start, end]; spread = blockIdx & 63 keeps the
-// recording atomics off one address
-__device__ unsigned long long g_tl[kTlSlots * kTlKernels * kTlSpread * 2];
-struct TLScope {
-    unsigned long long *rec;
-    __device__ TLScope(int k, uint32_t step)
-        : rec(&g_tl[(((step % kTlSlots) * kTlKernels + k) * kTlSpread + (blockIdx.x & 63u)) * 2])
-    {
-        if (threadIdx.x == 0) atomicMin(&rec[0], (unsigned long long)__builtin_amdgcn_s_memrealtime());
-    }
-    __device__ ~TLScope()
-    {
-        if (__lane_id() == 0) atomicMax(&rec[1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
-    }
-};
-#define TL_SCOPE(k, step) TLScope tl_scope_(k, step)
-#else
-#define TL_SCOPE(k, step) ((void)0)
-#endif
-
 constexpr int kWorldsPerBlock = 4;
 constexpr int kTileWorlds = 1024;             // worlds per scan tile (K2 block)
 
@@ -211,7 +172,6 @@ __device__ void world_step(SimState &S, const ObsTable &cur, WorldLDS &L, uint32
 
 __global__ __launch_bounds__(256, 8) void world_step_kernel(SimState S, ObsTable cur, int parity)
 {
-    TL_SCOPE(0, S.tl_step);
     __shared__ WorldLDS lds[kWorldsPerBlock];
     __shared__ int32_t blk[kWorldsPerBlock][5];
     const uint32_t wv = threadIdx.x >> 6;
@@ -238,13 +198,6 @@ __device__ void world_step(SimState &S, const ObsTable &cur, WorldLDS &L, uint32
     const uint32_t cap = S.cap;
     const size_t base = (size_t)w * cap;
     const int n0 = uniform(S.n[w]);
-#ifdef MB_PROF
-    unsigned long long prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    unsigned long long tp = PROF_NOW(), tq;
-#define KPROF(k) (tq = PROF_NOW(), prof[k] += tq - tp, tp = tq)
-#else
-#define KPROF(k) ((void)0)
-#endif
 
     // ---- stage the world in LDS; slot `lane`'s action row is fetched now and
     // consumed after addFood (its latency hides behind that serial phase) ----
@@ -305,7 +258,6 @@ __device__ void world_step(SimState &S, const ObsTable &cur, WorldLDS &L, uint32
     if (lane < kNumSpecies) { L.cnt[lane] = 0u; L.hsum[lane] = 0u; L.scount[lane] = 0; }
     if (lane == 0) L.consumed = 0;
     wave_sync();
-    KPROF(0);
 
     // ---- addFoodSystem (sim.cpp:363-387) + addFoodToChunk (:308-361) ----
     // The serial draw sequence uses at most 2 + 3 x 7 = 23 counters: lane k
@@ -341,7 +293,6 @@ __device__ void world_step(SimState &S, const ObsTable &cur, WorldLDS &L, uint32
         }
         ctr += k;
     }
-    KPROF(1);
 
     // ---- actionSystem (sim.cpp:419-502) ----
     for (int i = lane; i < n0; i += 64) {
@@ -385,7 +336,6 @@ __device__ void world_step(SimState &S, const ObsTable &cur, WorldLDS &L, uint32
         L.flags[i] = (uint8_t)fl;
     }
     wave_sync();
-    KPROF(2);
 
     // ---- healthSync (sim.cpp:505-581) ----
     // food: the k-th agent (slot order) standing on a cell takes the k-th live
@@ -460,7 +410,6 @@ __device__ void world_step(SimState &S, const ObsTable &cur, WorldLDS &L, uint32
         else n1 += made;
     }
     wave_sync();
-    KPROF(3);
     cur_food -= L.consumed;
 
     // ---- updateSurroundingObservation (sim.cpp:583-654) + tracker (:719-734) ----
@@ -516,7 +465,6 @@ __device__ void world_step(SimState &S, const ObsTable &cur, WorldLDS &L, uint32
     int n2 = n1 + total_need;
     if (n2 > (int)cap) { ovf += (uint32_t)(n2 - (int)cap); n2 = (int)cap; }
     wave_sync();
-    KPROF(4);
 
     // ---- compaction (SortArchetypeNode<Agent, WorldID>, sim.cpp:1129) ----
     int nn = 0;
@@ -549,16 +497,6 @@ __device__ void world_step(SimState &S, const ObsTable &cur, WorldLDS &L, uint32
         S.cur_food[w] = cur_food;
         if (ovf) S.overflow[w] += ovf;
     }
-    KPROF(5);
-#ifdef MB_PROF
-    prof[6] = (unsigned long long)n0;
-    prof[7] = 1;
-    if (lane < 8) {
-        unsigned long long v = 0;
-        for (int k = 0; k < 8; ++k) v = (int)lane == k ? prof[k] : v;
-        atomicAdd(&g_kprof[(blockIdx.x & 63u) * 8 + lane], v);
-    }
-#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -582,7 +520,6 @@ __device__ __forceinline__ int wave_incl_scan(int v)
 
 __global__ __launch_bounds__(1024) void scan_kernel(SimState S, int parity)
 {
-    TL_SCOPE(1, S.tl_step);
     __shared__ int32_t s_pre[5], s_tot[5];
     __shared__ int32_t s_wave[16][5];
     const int t = threadIdx.x, b = blockIdx.x;
@@ -644,7 +581,9 @@ __global__ __launch_bounds__(1024) void scan_kernel(SimState S, int parity)
             for (int k = 0; k < 5; ++k)
                 __hip_atomic_store(S.totals_host + k, k ? (uint32_t)s_tot[k - 1] : (uint32_t)s_tot[4],
                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            // (the dispatch's completion signal releases at system scope)
+            // make the mirror visible before the dispatch's completion signal,
+            // whatever scope the runtime gives that signal's release
+            __threadfence_system();
         }
     }
 }
@@ -686,7 +625,6 @@ __global__ __launch_bounds__(1024) void tile_sum_kernel(SimState S, int parity)
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void export_rows_kernel(SimState S, ObsTable nxt, int init)
 {
-    TL_SCOPE(2, S.tl_step);
     const uint32_t wv = threadIdx.x >> 6;
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t w = uniform(blockIdx.x * kWorldsPerBlock + wv);
@@ -807,18 +745,16 @@ __device__ __forceinline__ void move_rows(const uint32_t *totals, const int32_t 
 }
 
 __global__ __launch_bounds__(256) void move_kernel(const uint32_t *totals, const int32_t *src_of,
-                                                   MoveArgs args, uint32_t tl_step)
+                                                   MoveArgs args)
 {
-    TL_SCOPE(4, tl_step);
     move_rows(totals, src_of, args);
 }
 
 // the fused shift (DESIGN.md "Deferred Prev moves"): Action / HiddenState
 // gathered from the other half into both the current and the Prev column
 __global__ __launch_bounds__(256) void shift_move_kernel(const uint32_t *totals, const int32_t *src_of,
-                                                         MoveArgs args, uint32_t tl_step)
+                                                         MoveArgs args)
 {
-    TL_SCOPE(5, tl_step);
     move_rows(totals, src_of, args);
 }
 
@@ -848,9 +784,6 @@ __global__ __launch_bounds__(256) void shift_move_kernel(const uint32_t *totals,
 // ---------------------------------------------------------------------------
 #ifndef MB_KEY_AGENTS
 #define MB_KEY_AGENTS 8
-#endif
-#ifndef MB_ABL
-#define MB_ABL 0   // timing ablations: 1 no sensor work, 8 no output, 16 no survivors, 32 no pixel tests, 64 no wide pairs
 #endif
 constexpr int kKeyAgents = MB_KEY_AGENTS;     // agents per chunk (key rows)
 constexpr int kKeyStride = 36;                // key row: 32 pixels, finder, pad (16-B rows)
@@ -898,7 +831,6 @@ __device__ __forceinline__ void pair_fl(const SensorLDS &L, int nf, int i, int j
 // each half also takes the finder ray)
 __device__ __forceinline__ void run_wide(SensorLDS &L, int nf, int cnt)
 {
-    if (MB_ABL & (32 | 64)) return;
     const int lane = (int)__lane_id();
     for (int e0 = 0; e0 < cnt; e0 += 2) {
         const int e = e0 + (lane >> 5);
@@ -919,10 +851,8 @@ __device__ __forceinline__ void run_wide(SensorLDS &L, int nf, int cnt)
 
 // P2: survivors [q0, q0 + cnt): approximate roots bound the candidate pixels;
 // <= 2 pixels + the finder are tested inline, wider pairs go to the wide list
-__device__ __forceinline__ void run_survivors(SensorLDS &L, int nf, int a0, int q0, int cnt,
-                                              unsigned long long &nwide)
+__device__ __forceinline__ void run_survivors(SensorLDS &L, int nf, int a0, int q0, int cnt)
 {
-    if (MB_ABL & 16) return;
     const int lane = (int)__lane_id();
     bool wide = false;
     uint32_t code = 0;
@@ -951,7 +881,7 @@ __device__ __forceinline__ void run_survivors(SensorLDS &L, int nf, int a0, int 
             const int k1 = min((int)floorf(hi), kmax);
             const int c = k1 - k0 + 1;
             k0 += fwd ? 0 : 24;
-            if (!(MB_ABL & 32)) {
+            {
                 // the two edge pixels of [k0, k0 + c) get the exact predicate;
                 // interior pixels lie >= one pixel pitch minus kUEps (>= 0.08 in
                 // u) inside the root interval of a pair with r > 1, |f| > 1.5,
@@ -961,17 +891,13 @@ __device__ __forceinline__ void run_survivors(SensorLDS &L, int nf, int a0, int 
                 const int kl = k0 + max(c - 1, 0);
                 const float ua = L.u[k0 & 31], ub = L.u[kl & 31];
                 const uint32_t kin = zkey(fwd ? f - 1.0f : -f - 1.0f, order);
-#if MB_ABL & 512
-                const bool ha = true, hb = true;
-#else
                 const bool ha = far_pixel_hit(f, l, ua, fwd), hb = far_pixel_hit(f, l, ub, fwd);
-#endif
                 // finder ray (u = 0) of a far pair: q(0) = l^2 - 1 <= 0 and f > 0
                 const bool hf = (l * l - 1.0f <= 0.0f) & fwd;
                 if ((c > 0) & ha) atomicMin(&kr[k0], kin);
                 if ((c > 1) & hb) atomicMin(&kr[kl], kin);
-                if (!(MB_ABL & 1024) && hf) atomicMin(&kr[kSensor], kin);
-                if (!(MB_ABL & 256)) for (int k = k0 + 1; k < kl; ++k) atomicMin(&kr[k], kin);
+                if (hf) atomicMin(&kr[kSensor], kin);
+                for (int k = k0 + 1; k < kl; ++k) atomicMin(&kr[k], kin);
             }
         }
     }
@@ -983,7 +909,6 @@ __device__ __forceinline__ void run_survivors(SensorLDS &L, int nf, int a0, int 
         L.wl[s] = l;
     }
     const int nw = __popcll(wm);
-    nwide += (unsigned long long)nw;
     if (nw > 0) {
         wave_sync();
         run_wide(L, nf, nw);
@@ -1041,7 +966,6 @@ constexpr int kSensorWorlds = MB_SENSOR_WPB;   // worlds (waves) per sensor bloc
 template <bool kDepth, int kSplit>
 __global__ __launch_bounds__(64 * kSensorWorlds, MB_SENSOR_BLOCKS) void sensor_kernel(SimState S, ObsTable nxt)
 {
-    TL_SCOPE(3, S.tl_step);
     __shared__ SensorLDS lds[kSensorWorlds];
     const uint32_t wv = threadIdx.x >> 6;
     const uint32_t lane = threadIdx.x & 63u;
@@ -1052,15 +976,10 @@ __global__ __launch_bounds__(64 * kSensorWorlds, MB_SENSOR_BLOCKS) void sensor_k
     if (w >= S.W) return;
     SensorLDS &L = lds[wv];
     constexpr bool depth = kDepth;
-#ifdef MB_PROF
-    unsigned long long prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-#endif
     if (lane < kSensor) L.u[lane] = kURay[lane];
     SensorPrefetch pf;
     sensor_prefetch(S, w, lane, pf);
-    [[maybe_unused]] unsigned long long wide_n = 0;
-    do {
-    [[maybe_unused]] const unsigned long long t_start = PROF_NOW();
+    {
     const size_t base = (size_t)w * S.cap;
     const SensorPrefetch cur = pf;
     const int n = cur.n;
@@ -1106,10 +1025,8 @@ __global__ __launch_bounds__(64 * kSensorWorlds, MB_SENSOR_BLOCKS) void sensor_k
         row_hi = sp == 1 ? rb.x + c1 + (int)rank_below(m1) : sp == 2 ? rb.y + c2 + (int)rank_below(m2)
                : sp == 3 ? rb.z + c3 + (int)rank_below(m3) : rb.w + c4 + (int)rank_below(m4);
     }
-    if (MB_ABL & 1) continue;
     const int nobj = nf + n;
     wave_sync();
-    PROF_ADD(0, PROF_NOW() - t_start);
 
     for (int a0 = kChunk0; a0 < n; a0 += kChunkStep) {
         const int nc = min(kKeyAgents, n - a0);
@@ -1141,25 +1058,18 @@ __global__ __launch_bounds__(64 * kSensorWorlds, MB_SENSOR_BLOCKS) void sensor_k
                 nq += __popcll(m);
                 if (nq >= 64) {
                     wave_sync();
-                    [[maybe_unused]] const unsigned long long ta = PROF_NOW();
-                    run_survivors(L, nf, a0, nq - 64, 64, wide_n);
-                    PROF_ADD(2, PROF_NOW() - ta);
-                    PROF_ADD(5, 64);
+                    run_survivors(L, nf, a0, nq - 64, 64);
                     nq -= 64;
                 }
             }
         }
         if (nq > 0) {
             wave_sync();
-            [[maybe_unused]] const unsigned long long ta = PROF_NOW();
-            run_survivors(L, nf, a0, 0, nq, wide_n);
-            PROF_ADD(2, PROF_NOW() - ta);
-            PROF_ADD(5, nq);
+            run_survivors(L, nf, a0, 0, nq);
         }
         wave_sync();
-        [[maybe_unused]] const unsigned long long to = PROF_NOW();
         // ---- output: keys vs walls; lane = (agent ci, pixels 4g .. 4g+3) ----
-        if (!(MB_ABL & 8)) {
+        {
             const int ci = (int)(lane >> 3), g = (int)(lane & 7u);
             const int cc = min(ci, nc - 1);
             const int i = a0 + cc;
@@ -1203,66 +1113,11 @@ __global__ __launch_bounds__(64 * kSensorWorlds, MB_SENSOR_BLOCKS) void sensor_k
             S.finder[base + i] = agent ? (int32_t)(order - kOrderAgent) : -1;
         }
         wave_sync();
-        PROF_ADD(3, PROF_NOW() - to);
     }
-#ifdef MB_PROF
-    prof[1] += wide_n;
-    prof[4] += PROF_NOW() - t_start;
-    prof[6] += (unsigned long long)n * (unsigned long long)(nf + n);
-    prof[7] += 1;
-#endif
-    } while (false);
-#ifdef MB_PROF
-    if (lane < 8) {
-        unsigned long long v = 0;
-        for (int k = 0; k < 8; ++k) v = (int)lane == k ? prof[k] : v;
-        atomicAdd(&g_sprof[(blockIdx.x & 63u) * 8 + lane], v);
     }
-#endif
 }
 
-#ifdef MB_TL
-// timeline dump: out[slot][kernel][start, end] (realtime ticks; min / max over
-// the spread); clears the record
-extern "C" __attribute__((visibility("default"))) int mbots_debug_timeline(unsigned long long *out)
-{
-    static unsigned long long buf[kTlSlots * kTlKernels * kTlSpread * 2];
-    if (hipDeviceSynchronize() != hipSuccess) return -1;
-    if (hipMemcpyFromSymbol(buf, HIP_SYMBOL(g_tl), sizeof(buf)) != hipSuccess) return -1;
-    for (int i = 0; i < kTlSlots * kTlKernels; ++i) {
-        unsigned long long lo = ~0ull, hi = 0ull;
-        for (int j = 0; j < kTlSpread; ++j) {
-            const unsigned long long a = buf[(i * kTlSpread + j) * 2], b = buf[(i * kTlSpread + j) * 2 + 1];
-            if (a && a < lo) lo = a;
-            if (b > hi) hi = b;
-        }
-        out[2 * i] = lo;
-        out[2 * i + 1] = hi;
-    }
-    for (int i = 0; i < kTlSlots * kTlKernels * kTlSpread; ++i) { buf[2 * i] = ~0ull; buf[2 * i + 1] = 0ull; }
-    if (hipMemcpyToSymbol(HIP_SYMBOL(g_tl), buf, sizeof(buf)) != hipSuccess) return -1;
-    return 0;
-}
-#endif
 
-#ifdef MB_PROF
-extern "C" __attribute__((visibility("default"))) int mbots_debug_sensor_prof(unsigned long long *out)
-{
-    static unsigned long long buf[64 * 8], zero[64 * 8];
-    if (hipDeviceSynchronize() != hipSuccess) return -1;
-    for (int t = 0; t < 2; ++t) {
-        const void *sym = t == 0 ? HIP_SYMBOL(g_sprof) : HIP_SYMBOL(g_kprof);
-        if (hipMemcpyFromSymbol(buf, sym, sizeof(buf)) != hipSuccess) return -1;
-        if (hipMemcpyToSymbol(sym, zero, sizeof(zero)) != hipSuccess) return -1;
-        for (int k = 0; k < 8; ++k) {
-            unsigned long long v = 0;
-            for (int b = 0; b < 64; ++b) v += buf[b * 8 + k];
-            out[t * 8 + k] = v;
-        }
-    }
-    return 0;
-}
-#endif
 
 // ---------------------------------------------------------------------------
 // Learner observation rows (learn/util.py:14-29 construct_obs):
@@ -1313,10 +1168,8 @@ __global__ __launch_bounds__(256) void construct_obs_kernel(const uint32_t *tota
 // A shift right after a step runs shift_move_kernel instead (the deferred
 // Action / HiddenState move fused with this copy).
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void shift_kernel(const uint32_t *totals, ObsTable t, int mode,
-                                                    uint32_t tl_step)
+__global__ __launch_bounds__(256) void shift_kernel(const uint32_t *totals, ObsTable t, int mode)
 {
-    TL_SCOPE(5, tl_step);
     const uint32_t N = totals[0];
     const bool eager = mode != kShiftRest, rest = mode != kShiftEager;
     const uint32_t g4 = rest ? (4u * N + 15u) >> 4 : 0u, g8 = rest ? (8u * N + 15u) >> 4 : 0u;
@@ -1394,7 +1247,6 @@ __global__ __launch_bounds__(256) void synthetic_actions_kernel(SimState S, ObsT
                                                                 uint32_t seed, uint32_t step,
                                                                 int write_hidden)
 {
-    TL_SCOPE(6, S.tl_step);
     const uint32_t wv = threadIdx.x >> 6;
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t w = uniform(blockIdx.x * kWorldsPerBlock + wv);
@@ -1507,35 +1359,30 @@ hipError_t launch_move(const SimState &S, const ObsTable &cur, const ObsTable &n
     // flight to stream
     const unsigned bx = k <= 4 ? (unsigned)MB_MOVE_BLOCKS : 512u;
     if (parts & kMoveAHShift)
-        hipLaunchKernelGGL(shift_move_kernel, dim3(bx, k), dim3(256), 0, st, S.totals, S.src_of, m, S.tl_step);
+        hipLaunchKernelGGL(shift_move_kernel, dim3(bx, k), dim3(256), 0, st, S.totals, S.src_of, m);
     else
-        hipLaunchKernelGGL(move_kernel, dim3(bx, k), dim3(256), 0, st, S.totals, S.src_of, m, S.tl_step);
+        hipLaunchKernelGGL(move_kernel, dim3(bx, k), dim3(256), 0, st, S.totals, S.src_of, m);
     return hipGetLastError();
 }
 hipError_t launch_sensor(const SimState &S, const ObsTable &nxt, hipStream_t st, hipEvent_t done)
 {
-    size_t pad = 0;
-#ifdef MB_KNOBS
-    // occupancy experiment: extra dynamic LDS per sensor block
-    if (const char *e = getenv("MBOTS_SENSOR_LDS_PAD")) pad = (size_t)atol(e);
-#endif
     const bool fixd = (S.flags & kFlagFixDepth) != 0;
     const dim3 blk(64 * kSensorWorlds);
     if (S.W <= (uint32_t)MB_SENSOR_SPLIT_MAX) {   // small: MB_SENSOR_SPLIT waves per world
         constexpr int kWpb = kSensorWorlds / MB_SENSOR_SPLIT;
         const dim3 grid((S.W + kWpb - 1) / kWpb);
-        if (fixd) hipExtLaunchKernelGGL((sensor_kernel<true, MB_SENSOR_SPLIT>), grid, blk, (uint32_t)pad, st, nullptr, done, 0u, S, nxt);
-        else hipExtLaunchKernelGGL((sensor_kernel<false, MB_SENSOR_SPLIT>), grid, blk, (uint32_t)pad, st, nullptr, done, 0u, S, nxt);
+        if (fixd) hipExtLaunchKernelGGL((sensor_kernel<true, MB_SENSOR_SPLIT>), grid, blk, 0u, st, nullptr, done, 0u, S, nxt);
+        else hipExtLaunchKernelGGL((sensor_kernel<false, MB_SENSOR_SPLIT>), grid, blk, 0u, st, nullptr, done, 0u, S, nxt);
     } else {
         const dim3 grid((S.W + kSensorWorlds - 1) / kSensorWorlds);
-        if (fixd) hipExtLaunchKernelGGL((sensor_kernel<true, 1>), grid, blk, (uint32_t)pad, st, nullptr, done, 0u, S, nxt);
-        else hipExtLaunchKernelGGL((sensor_kernel<false, 1>), grid, blk, (uint32_t)pad, st, nullptr, done, 0u, S, nxt);
+        if (fixd) hipExtLaunchKernelGGL((sensor_kernel<true, 1>), grid, blk, 0u, st, nullptr, done, 0u, S, nxt);
+        else hipExtLaunchKernelGGL((sensor_kernel<false, 1>), grid, blk, 0u, st, nullptr, done, 0u, S, nxt);
     }
     return hipGetLastError();
 }
 hipError_t launch_shift(const SimState &S, const ObsTable &t, int mode, hipStream_t st)
 {
-    hipLaunchKernelGGL(shift_kernel, dim3(4096), dim3(256), 0, st, S.totals, t, mode, S.tl_step);
+    hipLaunchKernelGGL(shift_kernel, dim3(4096), dim3(256), 0, st, S.totals, t, mode);
     return hipGetLastError();
 }
 hipError_t launch_synthetic_actions(const SimState &S, const ObsTable &t, uint32_t seed,

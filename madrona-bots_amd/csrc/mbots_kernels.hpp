@@ -38,7 +38,6 @@ struct SimState {
     int32_t *species_out, *obsrow_out, *n_out;
     uint64_t *food_out;
     uint32_t W, cap, A, world_offset, flags, seed, ntiles;
-    uint32_t tl_step;               // step counter (MB_TL timeline builds)
 };
 
 inline void swap_state(SimState &S)

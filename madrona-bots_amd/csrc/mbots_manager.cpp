@@ -212,14 +212,19 @@ int materialize_prev(mbots_handle *h, hipStream_t st)
 {
     if (h->six_pending[h->tb]) {   // a step's deferred move (no shift since)
         HIP_TRY(hipSetDevice(h->device));
-        HIP_TRY(mbots::launch_move(h->S, h->T[h->tb ^ 1], h->T[h->tb], h->six_lazy[h->tb] ? 1 : 0,
-                                   mbots::kMovePrev6, st));
+        const int rc = timed(h, MBOTS_TK_MOVE, st, [&] {
+            return mbots::launch_move(h->S, h->T[h->tb ^ 1], h->T[h->tb], h->six_lazy[h->tb] ? 1 : 0,
+                                      mbots::kMovePrev6, st);
+        });
+        if (rc) return rc;
         h->six_pending[h->tb] = false;
         return MBOTS_OK;
     }
     if (!h->prev_lazy[h->tb]) return MBOTS_OK;
     HIP_TRY(hipSetDevice(h->device));
-    HIP_TRY(mbots::launch_shift(h->S, h->T[h->tb], mbots::kShiftRest, st));
+    const int rc = timed(h, MBOTS_TK_MOVE, st,
+                         [&] { return mbots::launch_shift(h->S, h->T[h->tb], mbots::kShiftRest, st); });
+    if (rc) return rc;
     h->prev_lazy[h->tb] = false;
     return MBOTS_OK;
 }
@@ -231,7 +236,10 @@ int materialize_prev_ah(mbots_handle *h, hipStream_t st)
 {
     if (!h->ah_pending[h->tb]) return MBOTS_OK;
     HIP_TRY(hipSetDevice(h->device));
-    HIP_TRY(mbots::launch_move(h->S, h->T[h->tb ^ 1], h->T[h->tb], 0, mbots::kMovePrevAH, st));
+    const int rc = timed(h, MBOTS_TK_MOVE, st, [&] {
+        return mbots::launch_move(h->S, h->T[h->tb ^ 1], h->T[h->tb], 0, mbots::kMovePrevAH, st);
+    });
+    if (rc) return rc;
     h->ah_pending[h->tb] = false;
     return MBOTS_OK;
 }
@@ -242,7 +250,10 @@ int materialize_cur_ah(mbots_handle *h, hipStream_t st)
 {
     if (!h->cur_ah_pending[h->tb]) return MBOTS_OK;
     HIP_TRY(hipSetDevice(h->device));
-    HIP_TRY(mbots::launch_move(h->S, h->T[h->tb ^ 1], h->T[h->tb], 0, mbots::kMoveAH, st));
+    const int rc = timed(h, MBOTS_TK_MOVE, st, [&] {
+        return mbots::launch_move(h->S, h->T[h->tb ^ 1], h->T[h->tb], 0, mbots::kMoveAH, st);
+    });
+    if (rc) return rc;
     h->cur_ah_pending[h->tb] = false;
     return MBOTS_OK;
 }
@@ -253,7 +264,10 @@ int materialize_psem(mbots_handle *h, hipStream_t st)
 {
     if (!h->psem_pending[h->tb]) return MBOTS_OK;
     HIP_TRY(hipSetDevice(h->device));
-    HIP_TRY(mbots::launch_move(h->S, h->T[h->tb ^ 1], h->T[h->tb], 0, mbots::kMoveSensor, st));
+    const int rc = timed(h, MBOTS_TK_MOVE, st, [&] {
+        return mbots::launch_move(h->S, h->T[h->tb ^ 1], h->T[h->tb], 0, mbots::kMoveSensor, st);
+    });
+    if (rc) return rc;
     h->psem_pending[h->tb] = false;
     return MBOTS_OK;
 }
@@ -453,7 +467,6 @@ int mbots_step(mbots_handle *h, void *stream)
     HIP_TRY(hipSetDevice(h->device));
     hipStream_t st = as_stream(stream);
     h->last_stream = st;
-    h->S.tl_step = (uint32_t)h->steps;
     const mbots::ObsTable &cur = h->T[h->tb];
     const mbots::ObsTable &nxt = h->T[h->tb ^ 1];
     int rc;

@@ -24,12 +24,30 @@ def species_rows(counts):
     return counts.sum(dim=0).to(torch.int64)
 
 
+def reassemble(bufs, all_cnt):
+    """Learner-side reassembly: bufs[r] holds rank r's species-major rows
+    (padded), all_cnt [world, 4] the per-rank species row counts.  Returns the
+    rows in global (species, world, slot) order: per species s, rank 0's
+    species-s rows, then rank 1's, ... -- the table one device holding every
+    world would export."""
+    all_cnt = torch.as_tensor(all_cnt).cpu()
+    parts = []
+    for s in range(4):
+        for r, b in enumerate(bufs):
+            a = int(all_cnt[r, :s].sum())
+            parts.append(b[a:a + int(all_cnt[r, s])])
+    return torch.cat(parts)
+
+
 def gather_rollout(tensors, rows_per_species, dst=0, group=None):
     """tensors: name -> [N_r, ...] species-major rows of this rank (same N_r);
     rows_per_species: int64 [4] summing to N_r.  Returns name -> [sum N_r, ...]
-    in global species-major order on rank dst, None elsewhere."""
+    in global species-major order on rank dst, None elsewhere.  `dst` is a
+    rank within `group` (the default group: the global rank)."""
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
+    # torch.distributed.gather takes a global rank
+    dst_global = dst if group is None else dist.get_global_rank(group, dst)
     dev = next(iter(tensors.values())).device
     cnt = rows_per_species.to(device=dev, dtype=torch.int64).reshape(4)
     all_cnt = [torch.zeros_like(cnt) for _ in range(world)]
@@ -45,12 +63,7 @@ def gather_rollout(tensors, rows_per_species, dst=0, group=None):
         pad = torch.zeros((n_max,) + tuple(t.shape[1:]), dtype=t.dtype, device=dev)
         pad[:n] = t
         bufs = [torch.empty_like(pad) for _ in range(world)] if rank == dst else None
-        dist.gather(pad, bufs, dst=dst, group=group)
+        dist.gather(pad, bufs, dst=dst_global, group=group)
         if rank == dst:
-            parts = []
-            for s in range(4):
-                for r in range(world):
-                    a = int(all_cnt[r, :s].sum())
-                    parts.append(bufs[r][a:a + int(all_cnt[r, s])])
-            out[name] = torch.cat(parts)
+            out[name] = reassemble(bufs, all_cnt)
     return out
