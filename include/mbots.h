@@ -3,14 +3,14 @@
  *
  * This is the drop-in boundary for the reference's host surface:
  *   class Manager            src/entry/mgr.hpp:10-68
- *   Manager::Impl::make      src/entry/mgr.cpp:166-240
+ *   Manager::Impl::make      src/entry/mgr.cpp:98-172
  *   nanobind SimManager      src/entry/entry.cpp:16-45
  * Plain pointers, sizes and status codes only (no torch / HIP C++ types).
  * Every function returns MBOTS_OK (0) or a negative MBOTS_E* code; the text of
  * the last error on the calling thread is available from mbots_last_error().
  * Streams are passed as `void *` holding a hipStream_t (NULL = default stream).
  *
- * Ownership (mgr.cpp:138-144): the handle owns every device buffer; tensors
+ * Ownership (mgr.cpp:70-76): the handle owns every device buffer; tensors
  * returned by mbots_export are non-owning views that stay valid until the next
  * mbots_step (the export tables are double-buffered and swap on every step;
  * the reference's views are likewise shape-stale after step()).
@@ -84,7 +84,7 @@ enum mbots_dtype {
     MBOTS_DTYPE_FLOAT32 = 3
 };
 
-/* A non-owning 2-D device tensor view (madrona::py::Tensor, mgr.cpp:138-144). */
+/* A non-owning 2-D device tensor view (madrona::py::Tensor, mgr.cpp:70-76). */
 typedef struct mbots_tensor {
     void   *data;        /* device pointer                                  */
     int32_t dtype;       /* enum mbots_dtype                                */
@@ -94,27 +94,27 @@ typedef struct mbots_tensor {
 
 typedef struct mbots_handle mbots_handle;
 
-/* Manager::Manager / Impl::make (mgr.cpp:166-251).  Runs world init
+/* Manager::Manager / Impl::make (mgr.cpp:98-172, :180-183).  Runs world init
  * (Sim::Sim, sim.cpp:1232-1256) and the Init graph (sim.cpp:1050-1059). */
 int mbots_create(const mbots_config *cfg, mbots_handle **out);
-/* Manager::~Manager (mgr.cpp:253-255) */
+/* Manager::~Manager (mgr.cpp:185-187) */
 int mbots_destroy(mbots_handle *h);
 
-/* Manager::step (mgr.cpp:51-63, :257-260): Step + Sensor graphs, enqueued on
+/* Manager::step (mgr.cpp:51-63, :189-192): Step + Sensor graphs, enqueued on
  * `stream`.  Unlike the reference it does not block; mbots_num_agents and the
  * host-side offsets synchronise with the last step on demand. */
 int mbots_step(mbots_handle *h, void *stream);
-/* Manager::shiftObservations (mgr.cpp:65-68, :262-265) */
+/* Manager::shiftObservations (mgr.cpp:65-68, :194-197) */
 int mbots_shift_observations(mbots_handle *h, void *stream);
 
 /* SimBridge::totalNumAgents (sim.hpp:74-78, sim.cpp:992-993).  Waits for the
  * last step's counters. */
 int mbots_num_agents(mbots_handle *h, uint32_t *out);
-/* Manager::exportTensor / the 11 tensor accessors (mgr.cpp:70-76, :267-490) */
+/* Manager::exportTensor / the 11 tensor accessors (mgr.cpp:70-76, :199-422) */
 int mbots_export(mbots_handle *h, int32_t export_id, mbots_tensor *out);
-/* Manager::setAction (mgr.cpp:319-340): row = export row (species-major). */
+/* Manager::setAction (mgr.cpp:251-272): row = export row (species-major). */
 int mbots_set_action(mbots_handle *h, uint32_t row, const int32_t action[6]);
-/* Manager::agentOffsetForWorld (mgr.cpp:342-345) */
+/* Manager::agentOffsetForWorld (mgr.cpp:274-277) */
 int mbots_agent_offset_for_world(mbots_handle *h, uint32_t world, uint32_t *out);
 
 /* Learner observation rows (learn/util.py:14-29 construct_obs over every
@@ -134,9 +134,10 @@ int mbots_save_checkpoint(mbots_handle *h, void *host_dst, uint64_t bytes);
 int mbots_load_checkpoint(mbots_handle *h, const void *host_src, uint64_t bytes);
 /* Debug dump of one world (viewer replacement): host arrays of agent_capacity
  * rows -- (x, y, rot.w, rot.z) f32, (species, health, finder) i32 -- the 48
- * packed food records, and the live agent count. */
+ * packed food records, the food boxes' rotations ([5][48] 22-bit quarter-turn
+ * fractions; may be NULL) and the live agent count. */
 int mbots_world_state(mbots_handle *h, uint32_t world, float *xy_rwrz, int32_t *sp_hp_finder,
-                      uint64_t *food, int32_t *n_out);
+                      uint64_t *food, uint32_t *food_rot, int32_t *n_out);
 
 /* Build utilities (benchmark / test harness, not reference API):
  * identity-keyed synthetic action stream: one-hot(threefry(seed,step |

@@ -11,7 +11,7 @@
 
 namespace mbots {
 
-// src/sim/types.hpp:13-14, :78-80; src/entry/mgr.cpp:106-111
+// src/sim/types.hpp:13-14, :78-80; src/entry/mgr.cpp:104-113
 constexpr int kNumSpecies = 4;
 constexpr int kHidden = 16;
 constexpr int kSensor = 32;

@@ -281,9 +281,13 @@ __device__ void world_step(SimState &S, const ObsTable &cur, WorldLDS &L, uint32
                     if ((p & kPkgLive) == 0u) {
                         const uint32_t rx = (uint32_t)sample_i32(D(k++), 0, kChunkW);
                         const uint32_t ry = (uint32_t)sample_i32(D(k++), 0, kChunkW);
-                        if (lane == 0)
+                        // food entity rotation angleAxis(2 pi U, z) (sim.cpp:338-341):
+                        // its quarter-turn fraction, the low 22 bits of U's 24
+                        const uint32_t rot = (D(k++) >> 8) & 0x3FFFFFu;
+                        if (lane == 0) {
                             L.food[chunk * kMaxPkg + q] = (uint16_t)((rx & 15u) | ((ry & 15u) << 4) | kPkgLive);
-                        k += 1;   // food entity rotation draw (sim.cpp:338-341)
+                            S.food_rot[((size_t)w * kMaxPkg + q) * kNumChunks + chunk] = rot;
+                        }
                         cur_food += 1;
                         break;
                     }
@@ -788,19 +792,27 @@ __global__ __launch_bounds__(256) void shift_move_kernel(const uint32_t *totals,
 constexpr int kKeyAgents = MB_KEY_AGENTS;     // agents per chunk (key rows)
 constexpr int kKeyStride = 36;                // key row: 32 pixels, finder, pad (16-B rows)
 constexpr int kQueueCap = 128;                // P1 survivors (flushed at >= 64)
-constexpr int kWideCap = 64;                  // wide pairs of one survivor batch
 constexpr float kWedge = 1.41421356f + 0.05f; // |l| <= |f| + sqrt(2): necessary for |u| < 1
 constexpr float kUEps = 2e-3f;                // root-interval margin in u
+// food squares lie inside their circumscribed circle, radius sqrt 2 (1.42 with
+// margin): the wedge |l| <= |f| + sqrt(2) 1.42, candidate pixels from that
+// circle's roots when |f| > kFoodFar (the square then lies wholly on one side
+// of the camera plane), at most kFoodInline candidates tested inline
+constexpr float kFoodR2 = 1.42f * 1.42f;
+constexpr float kWedgeFood = 1.41421356f * 1.42f + 0.05f;
+constexpr float kFoodFar = 2.5f;
+constexpr int kFoodInline = 6;
 
 struct SensorLDS {
     float2 obj[kMaxFood + kMaxCap];           // positions: food, then agents
+    float2 frot[kMaxFood];                    // food squares' (cos, sin)
     float2 hd[kMaxCap];                       // agent headings
     int8_t sp[kMaxCap];
     alignas(16) uint32_t key[kKeyAgents * kKeyStride];
     uint32_t qcode[kQueueCap + 1];            // P1 survivors: agent | object << 11 (+ a
-                                              // sink slot for the branch-free write)
-    uint32_t wcode[kWideCap];                 // wide pairs: code, f, l
-    float wf[kWideCap], wl[kWideCap];
+                                              // sink slot for the branch-free write); a
+                                              // survivor batch's wide pairs are compacted
+                                              // into its own range
     alignas(16) float u[kSensor];
 };
 
@@ -827,23 +839,31 @@ __device__ __forceinline__ void pair_fl(const SensorLDS &L, int nf, int i, int j
     l = vx * h.y - vy * h.x;   // along r = (hy, -hx)
 }
 
-// W: wide pairs [0, cnt), two per wave (32 lanes each: rays 0..31, lane 0 of
-// each half also takes the finder ray)
-__device__ __forceinline__ void run_wide(SensorLDS &L, int nf, int cnt)
+// W: wide pairs qcode[q0, q0 + cnt), two per wave (32 lanes each: rays 0..31,
+// lane 0 of each half also takes the finder ray)
+__device__ __forceinline__ void run_wide(SensorLDS &L, int nf, int a0, int q0, int cnt)
 {
     const int lane = (int)__lane_id();
     for (int e0 = 0; e0 < cnt; e0 += 2) {
         const int e = e0 + (lane >> 5);
         if (e < cnt) {
-            const uint32_t code = L.wcode[e];
-            const float f = L.wf[e], l = L.wl[e];
+            const uint32_t code = L.qcode[q0 + e];
             const int ic = (int)(code & 0x1Fu), j = (int)(code >> 11);
-            const uint32_t order = order_of(nf, j);
+            float f, l;
+            uint32_t order;
+            pair_fl(L, nf, a0 + ic, j, f, l, order);
             uint32_t *kr = L.key + ic * kKeyStride;
             const int k = lane & 31;
-            const uint32_t kv = pixel_key(f, l, L.u[k], k < 24, order);
+            uint32_t kv, kf;
+            if (j < nf) {   // food square: every ray exactly
+                const FoodBox b = box_setup(f, l, L.frot[j], L.hd[a0 + ic]);
+                kv = box_hit(b, L.u[k], k < 24) ? zkey(box_z(b, k < 24), order) : kNoKey;
+                kf = box_hit(b, 0.0f, true) ? zkey(box_z(b, true), order) : kNoKey;
+            } else {
+                kv = pixel_key(f, l, L.u[k], k < 24, order);
+                kf = finder_key(f, l, order);
+            }
             if (kv != kNoKey) atomicMin(&kr[k], kv);
-            const uint32_t kf = finder_key(f, l, order);
             if ((k == 0) & (kf != kNoKey)) atomicMin(&kr[kSensor], kf);
         }
     }
@@ -862,17 +882,20 @@ __device__ __forceinline__ void run_survivors(SensorLDS &L, int nf, int a0, int 
         const int ic = (int)(code & 0x1Fu), j = (int)(code >> 11);
         uint32_t order;
         pair_fl(L, nf, a0 + ic, j, f, l, order);
+        const bool food = j < nf;
         const float r2 = f * f + l * l;
-        if (r2 <= 1.0f || fabsf(f) <= 1.5f) {
+        if (food ? fabsf(f) <= kFoodFar : (r2 <= 1.0f) | (fabsf(f) <= 1.5f)) {
             wide = true;
         } else {
             const bool fwd = f > 0.0f;
-            const float sq = __builtin_amdgcn_sqrtf(r2 - 1.0f);
+            // bounding circle: radius 1 (agents) / 1.42 (food squares)
+            const float R2 = food ? kFoodR2 : 1.0f;
+            const float sq = __builtin_amdgcn_sqrtf(food ? R2 * (r2 - R2) : r2 - 1.0f);
             const float lf = l * f;
-            // approximate roots u = (lf -+ sq) / (f^2 - 1), widened by kUEps, in
+            // approximate roots u = (lf -+ R sqrt(r^2 - R^2)) / (f^2 - R^2), widened by kUEps, in
             // pixel coordinates s = (u + 1) sc - 0.5 (pixel k at s = k)
             const float sc = fwd ? 12.0f : 4.0f;
-            const float sia = sc * __builtin_amdgcn_rcpf(f * f - 1.0f);
+            const float sia = sc * __builtin_amdgcn_rcpf(f * f - R2);
             // (FMA: an approximation bounded by the kUEps margin either way)
             const float lo = __builtin_fmaf(lf - sq, sia, fwd ? 12.0f * (1.0f - kUEps) - 0.5f : 4.0f * (1.0f - kUEps) - 0.5f);
             const float hi = __builtin_fmaf(lf + sq, sia, fwd ? 12.0f * (1.0f + kUEps) - 0.5f : 4.0f * (1.0f + kUEps) - 0.5f);
@@ -881,13 +904,25 @@ __device__ __forceinline__ void run_survivors(SensorLDS &L, int nf, int a0, int 
             const int k1 = min((int)floorf(hi), kmax);
             const int c = k1 - k0 + 1;
             k0 += fwd ? 0 : 24;
-            {
+            uint32_t *kr = L.key + ic * kKeyStride;
+            if (food) {
+                if (c > kFoodInline) {
+                    wide = true;
+                } else {
+                    // every candidate gets the exact test; a far square lies
+                    // wholly on its camera's side, so box_hit is the line test
+                    const FoodBox b = box_setup(f, l, L.frot[j], L.hd[a0 + ic]);
+                    const uint32_t kin = zkey(box_z(b, fwd), order);
+                    for (int k = k0; k < k0 + c; ++k)
+                        if (box_line_hit(b, L.u[k & 31])) atomicMin(&kr[k], kin);
+                    if (fwd & box_line_hit(b, 0.0f)) atomicMin(&kr[kSensor], kin);
+                }
+            } else {
                 // the two edge pixels of [k0, k0 + c) get the exact predicate;
                 // interior pixels lie >= one pixel pitch minus kUEps (>= 0.08 in
                 // u) inside the root interval of a pair with r > 1, |f| > 1.5,
                 // where the approximate roots are off by ~1e-6 and the float
                 // q(u) by < 1e-4: they are hits carrying the object's key
-                uint32_t *kr = L.key + ic * kKeyStride;
                 const int kl = k0 + max(c - 1, 0);
                 const float ua = L.u[k0 & 31], ub = L.u[kl & 31];
                 const uint32_t kin = zkey(fwd ? f - 1.0f : -f - 1.0f, order);
@@ -901,17 +936,13 @@ __device__ __forceinline__ void run_survivors(SensorLDS &L, int nf, int a0, int 
             }
         }
     }
+    // every lane read its code above: the wide ones compact in place
     const uint64_t wm = ballot64(wide);
-    if (wide) {
-        const int s = (int)rank_below(wm);
-        L.wcode[s] = code;
-        L.wf[s] = f;
-        L.wl[s] = l;
-    }
+    if (wide) L.qcode[q0 + (int)rank_below(wm)] = code;
     const int nw = __popcll(wm);
     if (nw > 0) {
         wave_sync();
-        run_wide(L, nf, nw);
+        run_wide(L, nf, a0, q0, nw);
         wave_sync();
     }
 }
@@ -919,6 +950,7 @@ __device__ __forceinline__ void run_survivors(SensorLDS &L, int nf, int a0, int 
 // the world's staged inputs, loaded as one batch of independent loads
 struct SensorPrefetch {
     uint64_t food;             // lane < 48: packed chunk record
+    uint32_t rot0;             // lane < 48: the chunk's package-0 rotation
     float x, y, rw, rz;        // lane < min(n, 64): agent slot `lane`
     int32_t sp;
     int n;
@@ -931,6 +963,7 @@ __device__ __forceinline__ void sensor_prefetch(const SimState &S, uint32_t w, u
     p.n = uniform(S.n[w]);
     p.rb = reinterpret_cast<const int4 *>(S.row_base)[w];
     p.food = lane < kNumChunks ? S.food[(size_t)w * kNumChunks + lane] : 0ull;
+    p.rot0 = lane < kNumChunks ? S.food_rot[(size_t)w * kNumPkg + lane] : 0u;
     // slots [0, min(cap, 64)), loaded without waiting for n (rows past n are
     // stale and never used)
     if (lane < S.cap) {
@@ -985,7 +1018,7 @@ __global__ __launch_bounds__(64 * kSensorWorlds, MB_SENSOR_BLOCKS) void sensor_k
     const int n = cur.n;
 
     // ---- live food packages in (chunk, package) order -> objects [0, nf) ----
-    const int nf = stage_food(cur.food, lane, L.obj);
+    const int nf = stage_food(cur.food, cur.rot0, S.food_rot + (size_t)w * kNumPkg, lane, L.obj, L.frot);
     // ---- agents -> objects [nf, nf + n) ----
     if ((int)lane < n) {
         float hx, hy;
@@ -1051,7 +1084,8 @@ __global__ __launch_bounds__(64 * kSensorWorlds, MB_SENSOR_BLOCKS) void sensor_k
                 // pair_fl's (f, l) up to an FMA rounding: the cull's margin
                 // (kWedge - sqrt 2 = 0.05) dwarfs it; survivors recompute exactly
                 const float f = __builtin_fmaf(vx, ah.x, vy * ah.y), l = __builtin_fmaf(vx, ah.y, -(vy * ah.x));
-                const bool keep = (j < nobj) & (j != self) & (a < nc) & (fabsf(l) <= fabsf(f) + kWedge);
+                const bool keep = (j < nobj) & (j != self) & (a < nc) &
+                                  (fabsf(l) <= fabsf(f) + (j < nf ? kWedgeFood : kWedge));
                 const uint64_t m = ballot64(keep);
                 // branch-free: culled lanes write the sink slot (+1 % step)
                 L.qcode[keep ? nq + (int)rank_below(m) : kQueueCap] = (uint32_t)a | ((uint32_t)j << 11);
@@ -1271,7 +1305,7 @@ __global__ __launch_bounds__(256) void synthetic_actions_kernel(SimState S, ObsT
     }
 }
 
-// sensorIndexTensor (mgr.cpp:309-317): world-major agent order -> export row
+// sensorIndexTensor (mgr.cpp:241-249): world-major agent order -> export row
 __global__ __launch_bounds__(256) void sensor_index_kernel(SimState S, int32_t *out)
 {
     const uint32_t wv = threadIdx.x >> 6;

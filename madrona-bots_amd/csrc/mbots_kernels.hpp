@@ -21,6 +21,7 @@ struct SimState {
     uint32_t *ctr;                  // [W] RNG counter
     uint2 *key;                     // [W] RNG key
     uint64_t *food;                 // [W][48] per chunk: 5 x (x | y << 4) bytes, live mask << 40
+    uint32_t *food_rot;             // [W][5][48] food box rotation (22-bit quarter turn) per package
     int32_t *cur_food;              // [W] Sim::currentNumFood
     float *sreward;                 // [W][4] SpeciesReward
     int32_t *scount;                // [W][4] SpeciesCount (exported)

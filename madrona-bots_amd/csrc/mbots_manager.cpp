@@ -170,6 +170,7 @@ size_t layout(mbots_handle *h, Arena &a)
     S.ctr = a.take<uint32_t>(W);
     S.key = a.take<uint2>(W);
     S.food = a.take<uint64_t>(W * kNumChunks);
+    S.food_rot = a.take<uint32_t>(W * kNumPkg);
     S.cur_food = a.take<int32_t>(W);
     S.sreward = a.take<float>(W * kNumSpecies);
     S.scount = a.take<int32_t>(W * kNumSpecies);
@@ -296,7 +297,7 @@ struct CkptHeader {
     uint32_t version, num_worlds, cap, A, world_offset, flags, seed, n_rows;
     uint64_t bytes;
 };
-constexpr uint32_t kCkptVersion = 1;
+constexpr uint32_t kCkptVersion = 2;
 
 struct Seg {
     void *p;
@@ -313,6 +314,7 @@ std::vector<Seg> ckpt_segments(mbots_handle *h, mbots::ObsTable &t, uint32_t n_r
         {S.species, rows * 4}, {S.health, rows * 4}, {S.finder, rows * 4}, {S.obsrow, rows * 4},
         {S.sur0, rows * 4}, {S.sur1, rows * 4}, {S.stats, rows * 4},
         {S.n, W * 4}, {S.ctr, W * 4}, {S.key, W * 8}, {S.food, W * kNumChunks * 8},
+        {S.food_rot, W * kNumPkg * 4},
         {S.cur_food, W * 4}, {S.sreward, W * kNumSpecies * 4}, {S.scount, W * kNumSpecies * 4},
         {S.row_base, W * kNumSpecies * 4}, {S.world_off, W * 4}, {S.overflow, W * 4},
         {S.totals, 8 * 4}, {S.agent_steps, 8},
@@ -605,7 +607,7 @@ int mbots_export(mbots_handle *h, int32_t id, mbots_tensor *out)
     case MBOTS_EXPORT_DONE: p = h->done_zeros; break;
     case MBOTS_EXPORT_POSITION: p = t.pos; dt = MBOTS_DTYPE_FLOAT32; cols = 2; break;
     case MBOTS_EXPORT_PREV_POSITION: p = t.ppos; dt = MBOTS_DTYPE_FLOAT32; cols = 2; break;
-    // int32 health bits exported as a float32 view (types.hpp:119-124, mgr.cpp:397-414; B.2)
+    // int32 health bits exported as a float32 view (types.hpp:119-124, mgr.cpp:329-346; B.2)
     case MBOTS_EXPORT_HEALTH: p = t.health; dt = MBOTS_DTYPE_FLOAT32; break;
     case MBOTS_EXPORT_PREV_HEALTH: p = t.phealth; dt = MBOTS_DTYPE_FLOAT32; break;
     case MBOTS_EXPORT_SURROUNDING: p = t.sur; dt = MBOTS_DTYPE_FLOAT32; cols = 2; break;
@@ -815,7 +817,7 @@ int mbots_load_checkpoint(mbots_handle *h, const void *src, uint64_t bytes)
 }
 
 int mbots_world_state(mbots_handle *h, uint32_t world, float *xy_rwrz, int32_t *sp_hp_finder,
-                      uint64_t *food, int32_t *n_out)
+                      uint64_t *food, uint32_t *food_rot, int32_t *n_out)
 {
     using namespace mbots;
     if (!h || !xy_rwrz || !sp_hp_finder || !food || !n_out) return fail(MBOTS_E_INVALID, "null argument");
@@ -837,6 +839,8 @@ int mbots_world_state(mbots_handle *h, uint32_t world, float *xy_rwrz, int32_t *
         for (size_t i = 0; i < cap; ++i) sp_hp_finder[i * 3 + c] = v[i];
     }
     HIP_TRY(hipMemcpy(food, S.food + (size_t)world * kNumChunks, kNumChunks * 8, hipMemcpyDeviceToHost));
+    if (food_rot)
+        HIP_TRY(hipMemcpy(food_rot, S.food_rot + (size_t)world * kNumPkg, kNumPkg * 4, hipMemcpyDeviceToHost));
     HIP_TRY(hipMemcpy(n_out, S.n + world, 4, hipMemcpyDeviceToHost));
     return MBOTS_OK;
 }

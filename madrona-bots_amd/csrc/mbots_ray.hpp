@@ -92,11 +92,89 @@ __device__ __forceinline__ uint32_t finder_key(float f, float l, uint32_t order)
     return (hit | near) ? key : kNoKey;
 }
 
-// live food packages of a world in (chunk, package) order -> put(s, nf, x, y)
-// for s in [0, nf); lane c (< 48) holds chunk c's packed record.  Returns nf
-// (== currentNumFood <= 30).
-template <typename Put>
-__device__ __forceinline__ int stage_food_with(uint64_t rec, uint32_t lane, Put put)
+// ---------------------------------------------------------------------------
+// Food: the cube_render.obj +-1 box rotated about z by its package's draw
+// (sim.cpp:332-341), seen by the horizontal rays as a rotated square (DESIGN.md
+// 3.6).  The rotation is kept as the 22-bit quarter-turn fraction of the draw
+// (the cube is symmetric under quarter turns); cos / sin are fixed Taylor
+// polynomials in plain float operations (host and device libm differ).
+// ---------------------------------------------------------------------------
+constexpr float kQuarterTurnUnit = 1.57079632679489662f / 4194304.0f;   // (pi/2) 2^-22
+
+__device__ __forceinline__ float2 food_cs(uint32_t q22)
+{
+    const float w = (float)q22 * kQuarterTurnUnit;
+    const float w2 = w * w;
+    const float s = w * (1.0f - w2 * (1.0f / 6.0f) *
+                                   (1.0f - w2 * (1.0f / 20.0f) *
+                                               (1.0f - w2 * (1.0f / 42.0f) *
+                                                           (1.0f - w2 * (1.0f / 72.0f) *
+                                                                       (1.0f - w2 * (1.0f / 110.0f))))));
+    const float c = 1.0f - w2 * 0.5f *
+                               (1.0f - w2 * (1.0f / 12.0f) *
+                                           (1.0f - w2 * (1.0f / 30.0f) *
+                                                       (1.0f - w2 * (1.0f / 56.0f) *
+                                                                   (1.0f - w2 * (1.0f / 90.0f) *
+                                                                               (1.0f - w2 * (1.0f / 132.0f))))));
+    return make_float2(c, s);
+}
+
+// A food square in an agent's frame: centre (f, l), unit axes (p, q) and
+// (-q, p).  Ray u is the line Y = u X; with S(v) = v.Y - u v.X the corners'
+// S are S(centre) +- S(axis 1) +- S(axis 2), so the line meets the square iff
+// |l - u f| <= |q - u p| + |p + u q|.  The square spans view depths
+// f -+ (|p| + |q|): wholly ahead of the camera plane it is seen by forward rays
+// only (mirrored behind); straddling it, by every ray when the origin is
+// inside (|m1|, |m2| <= 1, the origin in box coordinates), else on the side of
+// the chord, the sign of its slab entry.  Depth (one per object, as the
+// circles' f - 1): the nearest corner's, max(0, f - (|p| + |q|)) forward.
+struct FoodBox {
+    float f, l, p, q, ext;
+};
+
+__device__ __forceinline__ FoodBox box_setup(float f, float l, float2 cs, float2 h)
+{
+    FoodBox b;
+    b.f = f;
+    b.l = l;
+    b.p = cs.x * h.x + cs.y * h.y;
+    b.q = cs.x * h.y - cs.y * h.x;
+    b.ext = fabsf(b.p) + fabsf(b.q);
+    return b;
+}
+
+__device__ __forceinline__ bool box_line_hit(const FoodBox &b, float u)
+{
+    return fabsf(b.l - u * b.f) <= fabsf(b.q - u * b.p) + fabsf(b.p + u * b.q);
+}
+
+__device__ __forceinline__ float slab_lo(float m, float b)
+{
+    return b > 0.0f ? (m - 1.0f) / b : b < 0.0f ? (m + 1.0f) / b : -__builtin_inff();
+}
+
+__device__ __forceinline__ bool box_hit(const FoodBox &b, float u, bool fwd)
+{
+    if (!box_line_hit(b, u)) return false;
+    if (b.f - b.ext > 0.0f) return fwd;
+    if (b.f + b.ext < 0.0f) return !fwd;
+    const float m1 = b.f * b.p + b.l * b.q, m2 = b.l * b.p - b.f * b.q;
+    if (fabsf(m1) <= 1.0f && fabsf(m2) <= 1.0f) return true;
+    const float lo = fmax_std(slab_lo(m1, b.p + u * b.q), slab_lo(m2, u * b.p - b.q));
+    return fwd ? lo > 0.0f : lo < 0.0f;
+}
+
+__device__ __forceinline__ float box_z(const FoodBox &b, bool fwd)
+{
+    return zq(max0(fwd ? b.f - b.ext : -(b.f + b.ext)));
+}
+
+// live food packages of a world in (chunk, package) order -> objects [0, nf):
+// position and the box's (cos, sin).  Lane c (< 48) holds chunk c's packed
+// record and package 0's rotation (rot0, prefetched; the others are loaded
+// here from rot_w = food_rot + w * 5 * 48).  Returns nf (== currentNumFood <= 30).
+__device__ __forceinline__ int stage_food(uint64_t rec, uint32_t rot0, const uint32_t *rot_w,
+                                          uint32_t lane, float2 *obj, float2 *frot)
 {
     const uint32_t live = (uint32_t)(rec >> 40) & 31u;
     const int cnt = __popc(live);
@@ -114,17 +192,14 @@ __device__ __forceinline__ int stage_food_with(uint64_t rec, uint32_t lane, Put 
     for (int k = 0; k < kMaxPkg; ++k) {
         if ((live >> k) & 1u) {
             const uint32_t xy = (uint32_t)(rec >> (8 * k)) & 0xFFu;
-            if (s < kMaxFood)   // live packages == currentNumFood <= 30
-                put(s, min(tot, kMaxFood), (float)(xy & 15u) + bx, (float)(xy >> 4) + by);
+            if (s < kMaxFood) {   // live packages == currentNumFood <= 30
+                obj[s] = make_float2((float)(xy & 15u) + bx, (float)(xy >> 4) + by);
+                frot[s] = food_cs(k == 0 ? rot0 : rot_w[k * kNumChunks + lane]);
+            }
             ++s;
         }
     }
     return min(tot, kMaxFood);
-}
-
-__device__ __forceinline__ int stage_food(uint64_t rec, uint32_t lane, float2 *obj)
-{
-    return stage_food_with(rec, lane, [&](int s, int, float x, float y) { obj[s] = make_float2(x, y); });
 }
 
 }  // namespace mbots

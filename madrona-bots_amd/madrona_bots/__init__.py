@@ -11,7 +11,7 @@ Mirrors the nanobind surface of src/entry/entry.cpp:16-45:
 
 Each accessor returns a ``Tensor`` whose ``to_torch()`` is a zero-copy torch
 view of device memory owned by the manager (madrona::py::Tensor,
-mgr.cpp:138-144).  The simulation runs in libmbots.so (hand-written gfx950
+mgr.cpp:70-76).  The simulation runs in libmbots.so (hand-written gfx950
 kernels); there is no CPU fallback -- importing without the built library
 raises ImportError.
 """
@@ -59,7 +59,7 @@ def _load():
         "mbots_checkpoint_size": [vp, P(ctypes.c_uint64)],
         "mbots_save_checkpoint": [vp, vp, ctypes.c_uint64],
         "mbots_load_checkpoint": [vp, vp, ctypes.c_uint64],
-        "mbots_world_state": [vp, u32, vp, vp, vp, P(i32)],
+        "mbots_world_state": [vp, u32, vp, vp, vp, vp, P(i32)],
         "mbots_export": [vp, i32, P(_CTensor)],
         "mbots_set_action": [vp, u32, P(i32)],
         "mbots_agent_offset_for_world": [vp, u32, P(u32)],
@@ -285,28 +285,32 @@ class SimManager:
     def world_state(self, world_idx):
         """Debug dump of one world (replacing the viewer's
         state readback): live agents' position, rotation (w, z), species,
-        health, finder slot, and the food packages (chunk, x, y) that are live,
+        health, finder slot, and the live food packages (chunk, x, y, rotation as
+        a 22-bit quarter-turn fraction),
         as numpy arrays (save with numpy.savez)."""
         import numpy as np
         cap = self.agent_capacity
         xyr = np.zeros((cap, 4), np.float32)
         shf = np.zeros((cap, 3), np.int32)
         food = np.zeros(48, np.uint64)
+        rot = np.zeros((5, 48), np.uint32)
         n = ctypes.c_int32()
         _check(_lib.mbots_world_state(self._h, int(world_idx), ctypes.c_void_p(xyr.ctypes.data),
                                       ctypes.c_void_p(shf.ctypes.data),
-                                      ctypes.c_void_p(food.ctypes.data), ctypes.byref(n)))
+                                      ctypes.c_void_p(food.ctypes.data),
+                                      ctypes.c_void_p(rot.ctypes.data), ctypes.byref(n)))
         k = n.value
         pk = []
         for c, rec in enumerate(food.tolist()):
             for q in range(5):
                 if (rec >> (40 + q)) & 1:
                     xy = (rec >> (8 * q)) & 0xFF
-                    pk.append((c, (c % 8) * 16 + (xy & 15), (c // 8) * 16 + (xy >> 4)))
+                    pk.append((c, (c % 8) * 16 + (xy & 15), (c // 8) * 16 + (xy >> 4),
+                               int(rot[q, c])))
         return {"position": xyr[:k, :2].copy(), "rotation_wz": xyr[:k, 2:].copy(),
                 "species": shf[:k, 0].copy(), "health": shf[:k, 1].copy(),
                 "finder": shf[:k, 2].copy(),
-                "food": np.array(pk, np.int32).reshape(-1, 3)}
+                "food": np.array(pk, np.int32).reshape(-1, 4)}
 
     def dump_worlds(self, path, worlds):
         """Write world_state() of each world in `worlds` to one .npz

@@ -17,7 +17,7 @@
 
 /* ------------------------------------------------------------------------ */
 /* Counter RNG.  Madrona's rand::initKey/split_i/RNG (sim.cpp:1238-1239,     */
-/* mgr.cpp:173) is not vendored; the build uses Threefry-2x32-20 (Random123)  */
+/* mgr.cpp:105) is not vendored; the build uses Threefry-2x32-20 (Random123)  */
 /* with the same call structure: world key = split(initKey(seed), 0, world),  */
 /* one 32-bit draw per counter value.                                         */
 /* ------------------------------------------------------------------------ */
@@ -82,6 +82,7 @@ typedef struct {
     uint8_t pkg_x[ORC_NUM_CHUNKS][ORC_MAX_PKG];
     uint8_t pkg_y[ORC_NUM_CHUNKS][ORC_MAX_PKG];
     uint32_t pkg_n[ORC_NUM_CHUNKS][ORC_MAX_PKG];
+    uint32_t pkg_rot[ORC_NUM_CHUNKS][ORC_MAX_PKG];  /* food entity rotation, 22-bit quarter turn */
     uint32_t num_agents[ORC_NUM_CHUNKS];    /* ChunkInfo::numAgents           */
     uint32_t total_speed[ORC_NUM_CHUNKS];   /* ChunkInfo::totalSpeed          */
     int32_t n;
@@ -241,7 +242,10 @@ static int add_food_to_chunk(orc_world *w, int chunk)
             w->pkg_x[chunk][i] = (uint8_t)rx;
             w->pkg_y[chunk][i] = (uint8_t)ry;
             w->pkg_n[chunk][i] = 1;
-            (void)sample_uniform(w);        /* food entity rotation, sim.cpp:338-341 */
+            /* food entity rotation angleAxis(2 pi U, z) (sim.cpp:338-341): the
+             * cube is symmetric under quarter turns, so 4U mod 1 -- the low 22
+             * bits of U's 24 -- fixes it */
+            w->pkg_rot[chunk][i] = (draw(w) >> 8) & 0x3FFFFFu;
             return 1;
         }
         /* numFood < kMaxFoodPerPackage (=1) never holds for a full package */
@@ -512,13 +516,14 @@ static void world_phase_c(orc_sim *s, uint32_t wi)
 /* Sensor (Madrona RenderingSystem raycast; build-defined spec)*/
 /*                                                                           */
 /* 32 pinhole pixels per agent (24 forward over the 90-degree FOV, 8 backward,*/
-/* gfx.cpp:252-253) plus the forward centre "finder" ray.  Every object (live */
-/* food package, other agent) is a unit circle; in the agent's frame (f along */
-/* the heading h, l along r = (hy, -hx)) the ray direction h + u r meets the  */
-/* circle iff q(u) = (A u - 2 l f) u + C <= 0 with A = f^2 - 1, C = l^2 - 1,  */
-/* and the hit lies ahead of the ray iff f + u l > 0 (backward camera: < 0).  */
-/* Depth is view-space z: z = f - 1 (clamped at 0, 15-bit mantissa: zq) for  */
-/* circles, the ray's                                                        */
+/* gfx.cpp:252-253) plus the forward centre "finder" ray.  Other agents are   */
+/* unit circles; in the agent's frame (f along the heading h, l along         */
+/* r = (hy, -hx)) the ray direction h + u r meets a circle iff                */
+/* q(u) = (A u - 2 l f) u + C <= 0 with A = f^2 - 1, C = l^2 - 1, and the hit */
+/* lies ahead of the ray iff f + u l > 0 (backward camera: < 0).  Live food   */
+/* packages are rotated +-1 squares (raster_box below).  Depth is view-space  */
+/* z: z = f - 1 for circles, the nearest corner's for squares (clamped at 0,  */
+/* 15-bit mantissa: zq), the ray's                                           */
 /* exit from the inner arena rectangle for the walls.  Each pixel takes the   */
 /* lexicographic minimum of (z, order): walls 0, food 1 + k, agents 64 + slot.*/
 /* ------------------------------------------------------------------------ */
@@ -620,6 +625,82 @@ static void raster(orc_hit *hits, float ax, float ay, float hx, float hy, float 
     if (C <= 0.0f && f > 0.0f) consider(&hits[ORC_SENSOR], zf, order);
 }
 
+/* Food is the cube_render.obj +-1 box rotated about z by the package's draw
+ * (sim.cpp:332-341); a horizontal ray at the agent's height meets its square
+ * cross-section.  Rotation: quarter-turn fraction q (22 bits) -> angle
+ * w = q (pi/2) 2^-22, cos / sin by fixed Taylor polynomials (host and device
+ * libm differ; these are plain float operations, identical on both).       */
+static const float kQuarterTurnUnit = 1.57079632679489662f / 4194304.0f;   /* (pi/2) 2^-22 */
+
+static void food_cs(uint32_t q22, float *c, float *s)
+{
+    float w = (float)q22 * kQuarterTurnUnit;
+    float w2 = w * w;
+    *s = w * (1.0f - w2 * (1.0f / 6.0f) *
+                  (1.0f - w2 * (1.0f / 20.0f) *
+                       (1.0f - w2 * (1.0f / 42.0f) *
+                            (1.0f - w2 * (1.0f / 72.0f) * (1.0f - w2 * (1.0f / 110.0f))))));
+    *c = 1.0f - w2 * 0.5f *
+                    (1.0f - w2 * (1.0f / 12.0f) *
+                         (1.0f - w2 * (1.0f / 30.0f) *
+                              (1.0f - w2 * (1.0f / 56.0f) *
+                                   (1.0f - w2 * (1.0f / 90.0f) * (1.0f - w2 * (1.0f / 132.0f))))));
+}
+
+/* In the agent frame (f along h, l along r) the square has centre (f, l) and
+ * unit axes (p, q), (-q, p).  Ray u is the line Y = u X; with
+ * S(v) = v.Y - u v.X the corners' S are S(centre) +- S(axis 1) +- S(axis 2),
+ * so the line meets the square iff |l - u f| <= |q - u p| + |p + u q|.  The
+ * square spans view depths f -+ (|p| + |q|): wholly ahead of the camera plane
+ * it is hit by forward rays only (mirrored behind); straddling the plane, by
+ * every ray when the origin is inside it (|m1|, |m2| <= 1: the origin in box
+ * coordinates), else on the side of the chord, the sign of the slab entry
+ * max_i lo_i.  Depth (one per object, like the circles' f - 1): the nearest
+ * corner's view depth, max(0, f - (|p| + |q|)) forward, max(0, -(f + ...))
+ * backward. */
+static int box_line_hit(float f, float l, float p, float q, float u)
+{
+    return fabsf(l - u * f) <= fabsf(q - u * p) + fabsf(p + u * q);
+}
+
+/* slab of one box axis along direction (1, u): lower end of t, or -inf */
+static float slab_lo(float m, float b)
+{
+    if (b > 0.0f) return (m - 1.0f) / b;
+    if (b < 0.0f) return (m + 1.0f) / b;
+    return -INFINITY;
+}
+
+static int box_hit(float f, float l, float p, float q, float ext, float u, int fwd)
+{
+    if (!box_line_hit(f, l, p, q, u)) return 0;
+    if (f - ext > 0.0f) return fwd;
+    if (f + ext < 0.0f) return !fwd;
+    float m1 = f * p + l * q, m2 = l * p - f * q;
+    if (fabsf(m1) <= 1.0f && fabsf(m2) <= 1.0f) return 1;
+    float lo = fmax_std(slab_lo(m1, p + u * q), slab_lo(m2, u * p - q));
+    return fwd ? lo > 0.0f : lo < 0.0f;
+}
+
+static void raster_box(orc_hit *hits, float ax, float ay, float hx, float hy, float cx, float cy,
+                       uint32_t rot, uint32_t order)
+{
+    float vx = cx - ax, vy = cy - ay;
+    float f = vx * hx + vy * hy;
+    float l = vx * hy - vy * hx;
+    float c, s;
+    food_cs(rot, &c, &s);
+    float p = c * hx + s * hy;
+    float q = c * hy - s * hx;
+    float ext = fabsf(p) + fabsf(q);
+    float zf = zq(max0(f - ext)), zb = zq(max0(-(f + ext)));
+    for (int k = 0; k < ORC_SENSOR; ++k) {
+        int fwd = k < 24;
+        if (box_hit(f, l, p, q, ext, ray_u(k), fwd)) consider(&hits[k], fwd ? zf : zb, order);
+    }
+    if (box_hit(f, l, p, q, ext, 0.0f, 1)) consider(&hits[ORC_SENSOR], zf, order);
+}
+
 static inline uint8_t depth_u8(float t)
 {
     if (!(t < 255.0f)) return 255;
@@ -646,7 +727,7 @@ static void world_phase_d(orc_sim *s, uint32_t wi)
             for (int k = 0; k < ORC_MAX_PKG; ++k) {
                 if (w->pkg_n[c][k] == 0) continue;
                 float fx = (float)w->pkg_x[c][k] + bx, fy = (float)w->pkg_y[c][k] + by;
-                raster(hits, a->x, a->y, hx, hy, fx, fy, 1u + nf);
+                raster_box(hits, a->x, a->y, hx, hy, fx, fy, w->pkg_rot[c][k], 1u + nf);
                 nf += 1;
             }
         }
@@ -855,5 +936,33 @@ void orc_world_state(const orc_sim *s, uint32_t wi, float *xy, float *rot, int32
         if (species) species[i] = a->species;
         if (health) health[i] = a->health;
         if (finder) finder[i] = a->finder;
+    }
+}
+
+int32_t orc_world_food(const orc_sim *s, uint32_t wi, int32_t *out)
+{
+    const orc_world *w = &s->w[wi];
+    int32_t k = 0;
+    for (int ch = 0; ch < ORC_NUM_CHUNKS; ++ch)
+        for (int p = 0; p < ORC_MAX_PKG; ++p) {
+            if (w->pkg_n[ch][p] == 0) continue;
+            out[4 * k + 0] = ch;
+            out[4 * k + 1] = (ch % ORC_CHUNKS_X) * ORC_CHUNK_W + w->pkg_x[ch][p];
+            out[4 * k + 2] = (ch / ORC_CHUNKS_X) * ORC_CHUNK_W + w->pkg_y[ch][p];
+            out[4 * k + 3] = (int32_t)w->pkg_rot[ch][p];
+            ++k;
+        }
+    return k;
+}
+
+void orc_probe_box(float ax, float ay, float hx, float hy, float cx, float cy, uint32_t rot,
+                   uint8_t *hit, float *z)
+{
+    orc_hit hits[ORC_SENSOR + 1];
+    for (int k = 0; k <= ORC_SENSOR; ++k) { hits[k].z = INFINITY; hits[k].order = 0xFFFFFFFFu; }
+    raster_box(hits, ax, ay, hx, hy, cx, cy, rot, 1u);
+    for (int k = 0; k <= ORC_SENSOR; ++k) {
+        hit[k] = hits[k].order == 1u;
+        z[k] = hits[k].z;
     }
 }

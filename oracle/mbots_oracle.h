@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-/* src/sim/types.hpp:13-14, :78-80; src/entry/mgr.cpp:106-111 */
+/* src/sim/types.hpp:13-14, :78-80; src/entry/mgr.cpp:104-113 */
 #define ORC_NUM_SPECIES   4
 #define ORC_HIDDEN        16
 #define ORC_SENSOR        32
@@ -83,8 +83,16 @@ uint32_t orc_overflow(const orc_sim *s);
 void     orc_world_state(const orc_sim *s, uint32_t w, float *xy, float *rot,
                          int32_t *species, int32_t *health, int32_t *finder,
                          int32_t *n);
+/* live food packages of world w in (chunk, package) order: out[k] = (chunk,
+ * x, y, 22-bit rotation); returns their count (<= 240 entries of 4) */
+int32_t  orc_world_food(const orc_sim *s, uint32_t w, int32_t *out);
 
 /* exposed primitives for known-answer tests */
+/* one food box (centre (cx, cy), 22-bit rotation) seen from an agent at
+ * (ax, ay) with heading (hx, hy): hit[k] / depth z[k] per ray (32 pixels,
+ * the finder ray last) */
+void     orc_probe_box(float ax, float ay, float hx, float hy, float cx, float cy,
+                       uint32_t rot, uint8_t *hit, float *z);
 void     orc_threefry2x32(const uint32_t key[2], const uint32_t ctr[2],
                           uint32_t out[2]);
 float    orc_sample_uniform(uint32_t bits);

@@ -73,11 +73,15 @@ def lib():
         L.orc_overflow.restype = u32
         L.orc_overflow.argtypes = [vp]
         L.orc_world_state.argtypes = [vp, u32, vp, vp, vp, vp, vp, vp]
+        L.orc_world_food.restype = i32
+        L.orc_world_food.argtypes = [vp, u32, vp]
         L.orc_threefry2x32.argtypes = [vp, vp, vp]
         L.orc_sample_uniform.restype = ctypes.c_float
         L.orc_sample_uniform.argtypes = [u32]
         L.orc_sample_i32.restype = i32
         L.orc_sample_i32.argtypes = [u32, i32, i32]
+        f32 = ctypes.c_float
+        L.orc_probe_box.argtypes = [f32, f32, f32, f32, f32, f32, u32, vp, vp]
         L.orc_action_hash.restype = u32
         L.orc_action_hash.argtypes = [u32, u32, u32, u32]
         _LIB = L
@@ -90,6 +94,16 @@ def threefry2x32(key, ctr):
     o = (ctypes.c_uint32 * 2)()
     lib().orc_threefry2x32(k, c, o)
     return int(o[0]), int(o[1])
+
+
+def probe_box(agent, heading, centre, rot):
+    """Rays of one agent against one food box: (hit[33] bool, z[33] f32)."""
+    hit = np.zeros(33, np.uint8)
+    z = np.zeros(33, np.float32)
+    lib().orc_probe_box(float(agent[0]), float(agent[1]), float(heading[0]), float(heading[1]),
+                        float(centre[0]), float(centre[1]), int(rot), hit.ctypes.data,
+                        z.ctypes.data)
+    return hit.astype(bool), z
 
 
 class OracleSim:
@@ -160,7 +174,10 @@ class OracleSim:
         lib().orc_world_state(self._h, w, xy.ctypes.data, rot.ctypes.data, sp.ctypes.data,
                               hp.ctypes.data, fd.ctypes.data, ctypes.byref(n))
         k = n.value
-        return dict(xy=xy[:k], rot=rot[:k], species=sp[:k], health=hp[:k], finder=fd[:k])
+        food = np.zeros((240, 4), np.int32)
+        nf = int(lib().orc_world_food(self._h, w, food.ctypes.data))
+        return dict(xy=xy[:k], rot=rot[:k], species=sp[:k], health=hp[:k], finder=fd[:k],
+                    food=food[:nf].copy())
 
     def snapshot(self, include_prev=True):
         """Copy of every exported column (dict name -> array)."""

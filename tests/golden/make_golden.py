@@ -7,7 +7,8 @@
        loaded with torch.load(weights_only=True)): observation width 69 and
        action width 6 (learn/env.py:19, learn/util.py:23-28);
      * mesh extents (data/agent_render.obj, data/cube_render.obj, read as text)
-       behind the sensor's unit-circle objects.
+       behind the sensor objects (agents: unit circles; food: the +-1 cube as a
+     rotated square).
 2. oracle_w4_a32_s69.npz / oracle_w8_a4_s7_fixed.npz -- golden vectors of the
    CPU oracle (oracle/mbots_oracle.c, the parity checker): per-step SHA-256
    digests of every exported column after step() and after

@@ -84,7 +84,8 @@ def test_world_state_matches_oracle():
         assert np.array_equal(g["species"], o["species"])
         assert np.array_equal(g["health"], o["health"])
         assert np.array_equal(g["finder"], o["finder"])
-        assert g["food"].shape[1] == 3 and len(g["food"]) <= 30
+        assert len(g["food"]) <= 30
+        assert np.array_equal(g["food"], o["food"])   # (chunk, x, y, box rotation)
 
 
 @pytest.mark.gpu

@@ -1,4 +1,4 @@
-"""GPU: tensor views, shapes/dtypes of the reference accessors (mgr.cpp:267-490)."""
+"""GPU: tensor views, shapes/dtypes of the reference accessors (mgr.cpp:199-422)."""
 import numpy as np
 import pytest
 import torch

@@ -220,6 +220,54 @@ def test_prev_sensor_is_last_steps_sensor():
 
 
 def test_health_export_is_int_bits():
-    # health_tensor views int32 health as float32 (types.hpp:119-124, mgr.cpp:397-414)
+    # health_tensor views int32 health as float32 (types.hpp:119-124, mgr.cpp:329-346)
     h = np.array([100], np.int32).view(np.float32)[0]
     assert h == np.float32(1.4e-43)
+
+
+# ---- food boxes (the +-1 cube of sim.cpp:332-341, rotated) ----
+FWD = list(range(24))
+
+
+def _hit_pixels(hit):
+    return [k for k in range(33) if hit[k]]
+
+
+def test_food_box_axis_aligned_ahead():
+    # box centre 10 ahead, rotation 0: spans Y in [-1, 1] from X = 9, so the
+    # line Y = u X meets it iff |u| <= 1/9: pixels 11, 12 (u = -+1/24) + finder
+    hit, z = po.probe_box((20.0, 20.0), (1.0, 0.0), (30.0, 20.0), 0)
+    assert _hit_pixels(hit) == [11, 12, 32]
+    assert z[11] == z[12] == z[32] == 9.0          # nearest face at view depth 9
+
+
+def test_food_box_diagonal_is_wider_and_nearer():
+    # a quarter-turn fraction 1/2 (45 degrees): corners at sqrt 2 on the
+    # diagonals, |u| <= sqrt(2)/10 = 0.141 covers pixels 10..13 (u = -+0.125)
+    hit, z = po.probe_box((20.0, 20.0), (1.0, 0.0), (30.0, 20.0), 1 << 21)
+    assert _hit_pixels(hit) == [10, 11, 12, 13, 32]
+    assert abs(float(z[10]) - (10.0 - 2.0 ** 0.5)) < 1e-3
+    # rotation by a full quarter turn is the same square as rotation 0
+    hit_q, z_q = po.probe_box((20.0, 20.0), (1.0, 0.0), (30.0, 20.0), (1 << 22) - 1)
+    assert _hit_pixels(hit_q) == [11, 12, 32]
+
+
+def test_food_box_behind_uses_backward_camera():
+    # backward pixels 24..31 at u = (2k+1)/8 - 1: only the 45-degree box reaches
+    # |u| = 0.125 (pixels 27, 28); no forward pixel, no finder
+    hit, _ = po.probe_box((50.0, 20.0), (1.0, 0.0), (40.0, 20.0), 0)
+    assert _hit_pixels(hit) == []
+    hit, z = po.probe_box((50.0, 20.0), (1.0, 0.0), (40.0, 20.0), 1 << 21)
+    assert _hit_pixels(hit) == [27, 28]
+    assert abs(float(z[27]) - (10.0 - 2.0 ** 0.5)) < 1e-3
+
+
+def test_food_box_containing_the_agent_fills_every_ray():
+    hit, z = po.probe_box((20.3, 20.2), (0.6, 0.8), (20.0, 20.0), 12345)
+    assert hit.all() and (z == 0.0).all()
+
+
+def test_food_box_rotation_follows_heading_frame():
+    # heading +y: a box 10 ahead along +y behaves like the +x case
+    hit, z = po.probe_box((20.0, 20.0), (0.0, 1.0), (20.0, 30.0), 0)
+    assert _hit_pixels(hit) == [11, 12, 32] and z[11] == 9.0
