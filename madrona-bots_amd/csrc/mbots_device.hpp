@@ -11,6 +11,13 @@
 
 namespace mbots {
 
+// host + device: the world-step math shared by the HIP kernels and the CPU
+// execution mode (mbots_cpu.cpp), compiled once per side with -ffp-contract=off
+#define MB_HD __host__ __device__ __forceinline__
+
+MB_HD uint32_t f2u(float x) { return __builtin_bit_cast(uint32_t, x); }
+MB_HD float u2f(uint32_t x) { return __builtin_bit_cast(float, x); }
+
 // src/sim/types.hpp:13-14, :78-80; src/entry/mgr.cpp:104-113
 constexpr int kNumSpecies = 4;
 constexpr int kHidden = 16;
@@ -34,12 +41,12 @@ constexpr float kRotS = 0.04997916927067833f;
 // Counter RNG: Threefry-2x32-20 (Random123).  Stands in for Madrona's
 // rand::split_i / RNG (sim.cpp:1238-1239); KAT-checked in tests.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t rotl32(uint32_t x, uint32_t r)
+MB_HD uint32_t rotl32(uint32_t x, uint32_t r)
 {
     return (x << r) | (x >> (32u - r));
 }
 
-__device__ __forceinline__ uint2 threefry2x32(uint32_t k0, uint32_t k1, uint32_t c0, uint32_t c1)
+MB_HD uint2 threefry2x32(uint32_t k0, uint32_t k1, uint32_t c0, uint32_t c1)
 {
     const uint32_t k2 = 0x1BD11BDAu ^ k0 ^ k1;
     uint32_t x0 = c0 + k0, x1 = c1 + k1;
@@ -53,12 +60,12 @@ __device__ __forceinline__ uint2 threefry2x32(uint32_t k0, uint32_t k1, uint32_t
     return make_uint2(x0, x1);
 }
 
-__device__ __forceinline__ float u01(uint32_t bits)
+MB_HD float u01(uint32_t bits)
 {
     return (float)(bits >> 8) * (1.0f / 16777216.0f);
 }
 
-__device__ __forceinline__ int32_t sample_i32(uint32_t bits, int32_t a, int32_t b)
+MB_HD int32_t sample_i32(uint32_t bits, int32_t a, int32_t b)
 {
     uint32_t range = (uint32_t)(b - a);
     return a + (int32_t)(((uint64_t)bits * (uint64_t)range) >> 32);
@@ -67,11 +74,11 @@ __device__ __forceinline__ int32_t sample_i32(uint32_t bits, int32_t a, int32_t 
 // ---------------------------------------------------------------------------
 // Math shared by the action and sensor phases
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ float fmin_std(float a, float b) { return (b < a) ? b : a; }
-__device__ __forceinline__ float fmax_std(float a, float b) { return (a < b) ? b : a; }
+MB_HD float fmin_std(float a, float b) { return (b < a) ? b : a; }
+MB_HD float fmax_std(float a, float b) { return (a < b) ? b : a; }
 
 // Sim::getChunkIndex (sim.inl:49-62)
-__device__ __forceinline__ int32_t chunk_index(float cx, float cy)
+MB_HD int32_t chunk_index(float cx, float cy)
 {
     int32_t x = (int32_t)cx, y = (int32_t)cy;
     if (x < 0 || y < 0 || x >= kChunksX || y >= kChunksY) return -1;
@@ -79,7 +86,7 @@ __device__ __forceinline__ int32_t chunk_index(float cx, float cy)
 }
 
 // rot.rotateVec({1,0,0}).normalize() for a z-only quaternion (sim.cpp:466-468)
-__device__ __forceinline__ void heading(float w, float z, float &dx, float &dy)
+MB_HD void heading(float w, float z, float &dx, float &dy)
 {
     float vx = 1.0f - 2.0f * (z * z);
     float vy = 2.0f * (z * w);
@@ -91,7 +98,7 @@ __device__ __forceinline__ void heading(float w, float z, float &dx, float &dy)
 // ---------------------------------------------------------------------------
 // Sensor output quantisation
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ uint8_t depth_u8(float t)
+MB_HD uint8_t depth_u8(float t)
 {
     if (!(t < 255.0f)) return 255;
     return (uint8_t)(int32_t)t;

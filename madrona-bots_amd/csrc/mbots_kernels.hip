@@ -802,6 +802,7 @@ constexpr float kFoodR2 = 1.42f * 1.42f;
 constexpr float kWedgeFood = 1.41421356f * 1.42f + 0.05f;
 constexpr float kFoodFar = 2.5f;
 constexpr int kFoodInline = 6;
+constexpr float kFarCull = 5.0f;               // P1 angular cull from this |f| on
 
 struct SensorLDS {
     float2 obj[kMaxFood + kMaxCap];           // positions: food, then agents
@@ -816,10 +817,11 @@ struct SensorLDS {
     alignas(16) float u[kSensor];
 };
 
-// pinhole offsets (IEEE constant folding == the oracle's runtime division)
+// pinhole offsets u = (2k + 1) / 24 - 1 forward, (2k' + 1) / 8 - 1 backward,
+// as the oracle's one rounding (2k - 23) (1/24) / exact (2k' - 7) / 8
 constexpr float u_of(int k)
 {
-    return k < 24 ? (float)(2 * k + 1) / 24.0f - 1.0f : (float)(2 * (k - 24) + 1) / 8.0f - 1.0f;
+    return k < 24 ? (float)(2 * k - 23) * (1.0f / 24.0f) : (float)(2 * (k - 24) - 7) * 0.125f;
 }
 #define MB_U4(k) u_of(k), u_of(k + 1), u_of(k + 2), u_of(k + 3)
 __constant__ float kURay[kSensor] = {MB_U4(0),  MB_U4(4),  MB_U4(8),  MB_U4(12),
@@ -1084,8 +1086,30 @@ __global__ __launch_bounds__(64 * kSensorWorlds, MB_SENSOR_BLOCKS) void sensor_k
                 // pair_fl's (f, l) up to an FMA rounding: the cull's margin
                 // (kWedge - sqrt 2 = 0.05) dwarfs it; survivors recompute exactly
                 const float f = __builtin_fmaf(vx, ah.x, vy * ah.y), l = __builtin_fmaf(vx, ah.y, -(vy * ah.x));
-                const bool keep = (j < nobj) & (j != self) & (a < nc) &
-                                  (fabsf(l) <= fabsf(f) + (j < nf ? kWedgeFood : kWedge));
+                const bool food = j < nf;
+                const float af = fabsf(f);
+                bool keep = (j < nobj) & (j != self) & (a < nc) &
+                            (fabsf(l) <= af + (food ? kWedgeFood : kWedge));
+                {
+                    // a far pair (|f| >= kFarCull) also needs a pixel centre, or
+                    // forward the finder ray u = 0, within w of its centre's
+                    // offset u_c = l / f: w bounds the bounding circle's roots,
+                    // a (sqrt(1 + u_c^2) + a |u_c|) / (1 - a^2) with a = R / |f|
+                    // (<= 0.284 here), plus the rcp / FMA error margin (56 % of
+                    // the wedge's survivors go: step -3 %)
+                    const float rf = __builtin_amdgcn_rcpf(f);
+                    const float uc = l * rf;
+                    const float ar = (food ? 1.42f : 1.0f) * fabsf(rf);
+                    const float w = ar * __builtin_fmaf(ar, fabsf(uc), __builtin_fmaf(0.5f * uc, uc, 1.0f)) *
+                                    __builtin_fmaf(1.2f * ar, ar, 1.0f) * 1.001f + 1e-4f;
+                    const bool fwd = f > 0.0f;
+                    const float sc = fwd ? 12.0f : 4.0f;
+                    const float s = __builtin_fmaf(uc, sc, sc - 0.5f);
+                    const float sn = __builtin_rintf(fminf(fmaxf(s, 0.0f), fwd ? 23.0f : 7.0f));
+                    const bool pix = fabsf(s - sn) <= sc * w;
+                    const bool fin = fwd & (fabsf(uc) <= w);
+                    keep = keep & ((af < kFarCull) | pix | fin);
+                }
                 const uint64_t m = ballot64(keep);
                 // branch-free: culled lanes write the sink slot (+1 % step)
                 L.qcode[keep ? nq + (int)rank_below(m) : kQueueCap] = (uint32_t)a | ((uint32_t)j << 11);

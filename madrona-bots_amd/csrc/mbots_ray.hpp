@@ -16,22 +16,22 @@ constexpr float kInLo = 0.0f + 0.2f;          // inner arena rectangle (walls, s
 constexpr float kInHiX = 128.0f - 0.2f;
 constexpr float kInHiY = 96.0f - 0.2f;
 
-__device__ __forceinline__ float max0(float x) { return x > 0.0f ? x : 0.0f; }
-__device__ __forceinline__ float zq(float z) { return __uint_as_float(__float_as_uint(z) & ~0xFFu); }
-__device__ __forceinline__ uint32_t zkey(float z, uint32_t order)
+MB_HD float max0(float x) { return x > 0.0f ? x : 0.0f; }
+MB_HD float zq(float z) { return u2f(f2u(z) & ~0xFFu); }
+MB_HD uint32_t zkey(float z, uint32_t order)
 {
-    return (__float_as_uint(z) & ~0xFFu) | order;
+    return (f2u(z) & ~0xFFu) | order;
 }
 
 // predicates below use non-short-circuit & | so they compile to VALU selects,
 // not exec-mask branches; the float operations are the oracle's
-__device__ __forceinline__ bool inside_arena(float ox, float oy)
+MB_HD bool inside_arena(float ox, float oy)
 {
     return (ox >= kInLo) & (ox <= kInHiX) & (oy >= kInLo) & (oy <= kInHiY);
 }
 
 // wall depth of a ray: exit from the inner rectangle; 0 inside a wall box
-__device__ __forceinline__ float wall_z(float ox, float oy, float dx, float dy)
+MB_HD float wall_z(float ox, float oy, float dx, float dy)
 {
     if (!inside_arena(ox, oy)) return 0.0f;
     float tx = __builtin_inff(), ty = __builtin_inff();
@@ -46,20 +46,20 @@ __device__ __forceinline__ float wall_z(float ox, float oy, float dx, float dy)
 // object at view depth z hides the wall iff z * d < (X - o) per axis: for
 // d > 0 z * d < hi - o, for d < 0 z * d > lo - o, i.e. z * |d| < o - lo (IEEE
 // products and differences are sign-symmetric, so this is the same predicate)
-__device__ __forceinline__ bool beats_wall(float ox, float oy, float dx, float dy, float z)
+MB_HD bool beats_wall(float ox, float oy, float dx, float dy, float z)
 {
     const bool bx = (dx == 0.0f) | (z * fabsf(dx) < (dx > 0.0f ? kInHiX - ox : ox - kInLo));
     const bool by = (dy == 0.0f) | (z * fabsf(dy) < (dy > 0.0f ? kInHiY - oy : oy - kInLo));
     return inside_arena(ox, oy) & bx & by;
 }
 
-__device__ __forceinline__ uint32_t order_of(int nf, int j)
+MB_HD uint32_t order_of(int nf, int j)
 {
     return j < nf ? kOrderFood + (uint32_t)j : kOrderAgent + (uint32_t)(j - nf);
 }
 
 // exact predicate of (f, l) on pixel ray k < 32 with offset u; key or kNoKey
-__device__ __forceinline__ uint32_t pixel_key(float f, float l, float u, bool fwdk, uint32_t order)
+MB_HD uint32_t pixel_key(float f, float l, float u, bool fwdk, uint32_t order)
 {
     const float A = f * f - 1.0f, B2 = 2.0f * (l * f), C = l * l - 1.0f;
     const float q = (A * u - B2) * u + C;
@@ -74,7 +74,7 @@ __device__ __forceinline__ uint32_t pixel_key(float f, float l, float u, bool fw
 
 // pixel_key's hit test for a far pair (f^2 + l^2 > 1, |f| > 1.5: never "near";
 // its key is zkey(fwd ? f - 1 : -f - 1, order) on every pixel it hits)
-__device__ __forceinline__ bool far_pixel_hit(float f, float l, float u, bool fwdk)
+MB_HD bool far_pixel_hit(float f, float l, float u, bool fwdk)
 {
     const float A = f * f - 1.0f, B2 = 2.0f * (l * f), C = l * l - 1.0f;
     const float q = (A * u - B2) * u + C;
@@ -83,7 +83,7 @@ __device__ __forceinline__ bool far_pixel_hit(float f, float l, float u, bool fw
 }
 
 // the finder ray (u = 0)
-__device__ __forceinline__ uint32_t finder_key(float f, float l, uint32_t order)
+MB_HD uint32_t finder_key(float f, float l, uint32_t order)
 {
     const float C = l * l - 1.0f;
     const bool hit = (C <= 0.0f) & (f > 0.0f);
@@ -101,7 +101,7 @@ __device__ __forceinline__ uint32_t finder_key(float f, float l, uint32_t order)
 // ---------------------------------------------------------------------------
 constexpr float kQuarterTurnUnit = 1.57079632679489662f / 4194304.0f;   // (pi/2) 2^-22
 
-__device__ __forceinline__ float2 food_cs(uint32_t q22)
+MB_HD float2 food_cs(uint32_t q22)
 {
     const float w = (float)q22 * kQuarterTurnUnit;
     const float w2 = w * w;
@@ -132,7 +132,7 @@ struct FoodBox {
     float f, l, p, q, ext;
 };
 
-__device__ __forceinline__ FoodBox box_setup(float f, float l, float2 cs, float2 h)
+MB_HD FoodBox box_setup(float f, float l, float2 cs, float2 h)
 {
     FoodBox b;
     b.f = f;
@@ -143,17 +143,17 @@ __device__ __forceinline__ FoodBox box_setup(float f, float l, float2 cs, float2
     return b;
 }
 
-__device__ __forceinline__ bool box_line_hit(const FoodBox &b, float u)
+MB_HD bool box_line_hit(const FoodBox &b, float u)
 {
     return fabsf(b.l - u * b.f) <= fabsf(b.q - u * b.p) + fabsf(b.p + u * b.q);
 }
 
-__device__ __forceinline__ float slab_lo(float m, float b)
+MB_HD float slab_lo(float m, float b)
 {
     return b > 0.0f ? (m - 1.0f) / b : b < 0.0f ? (m + 1.0f) / b : -__builtin_inff();
 }
 
-__device__ __forceinline__ bool box_hit(const FoodBox &b, float u, bool fwd)
+MB_HD bool box_hit(const FoodBox &b, float u, bool fwd)
 {
     if (!box_line_hit(b, u)) return false;
     if (b.f - b.ext > 0.0f) return fwd;
@@ -164,7 +164,7 @@ __device__ __forceinline__ bool box_hit(const FoodBox &b, float u, bool fwd)
     return fwd ? lo > 0.0f : lo < 0.0f;
 }
 
-__device__ __forceinline__ float box_z(const FoodBox &b, bool fwd)
+MB_HD float box_z(const FoodBox &b, bool fwd)
 {
     return zq(max0(fwd ? b.f - b.ext : -(b.f + b.ext)));
 }

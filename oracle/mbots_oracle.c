@@ -531,10 +531,13 @@ static const float kInLo = 0.0f + 0.2f;     /* walls: makeWalls (sim.cpp:157-194
 static const float kInHiX = 128.0f - 0.2f;  /* 0.2-thick boxes on the boundary    */
 static const float kInHiY = 96.0f - 0.2f;
 
+/* pixel k's offset u = (2k + 1) / 24 - 1 (forward, k < 24) or
+ * (2(k - 24) + 1) / 8 - 1 (backward), as one rounding: (2k - 23) * (1/24),
+ * (2(k - 24) - 7) / 8 (exact) */
 static float ray_u(int k)
 {
-    if (k < 24) return (float)(2 * k + 1) / 24.0f - 1.0f;
-    return (float)(2 * (k - 24) + 1) / 8.0f - 1.0f;
+    if (k < 24) return (float)(2 * k - 23) * (1.0f / 24.0f);
+    return (float)(2 * (k - 24) - 7) * 0.125f;
 }
 
 /* ray direction k of heading (hx, hy) */

@@ -49,3 +49,25 @@ def test_set_action_and_offsets():
     assert offs[0] == 0 and all(b >= a for a, b in zip(offs, offs[1:]))
     si = m.sensor_index_tensor().to_torch().cpu().numpy().ravel()
     assert sorted(si.tolist()) == list(range(m.num_agents()))
+
+
+@pytest.mark.parametrize("worlds", [8, 1100])
+def test_offsets_and_sensor_index_match_oracle(worlds):
+    """agentOffsetForWorld (mgr.cpp:274-277) and sensorIndexTensor
+    (mgr.cpp:241-249) against the oracle's world counts and slot -> row map,
+    after several steps (deaths, births and respawns move both)."""
+    import madrona_bots as mb
+    import pyoracle
+    m = mb.SimManager(0, worlds, 69, 32)
+    o = pyoracle.OracleSim(worlds, 69, 32, num_threads=8)
+    for t in range(6):
+        m.write_synthetic_actions(1234, t, True)
+        o.write_synthetic_actions(1234, t, True)
+        m.step(); o.step()
+        m.shift_observations(); o.shift_observations()
+        counts, offsets = o.world_counts()
+        got = np.array([m.agent_offset_for_world(w) for w in range(worlds)])
+        assert np.array_equal(got, offsets), t
+        si = m.sensor_index_tensor().to_torch().cpu().numpy().ravel()
+        assert np.array_equal(si, o.sensor_index()), t
+        assert int(counts.sum()) == m.num_agents()
