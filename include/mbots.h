@@ -8,7 +8,8 @@
  * Plain pointers, sizes and status codes only (no torch / HIP C++ types).
  * Every function returns MBOTS_OK (0) or a negative MBOTS_E* code; the text of
  * the last error on the calling thread is available from mbots_last_error().
- * Streams are passed as `void *` holding a hipStream_t (NULL = default stream).
+ * Streams are passed as `void *` holding a hipStream_t (NULL = default stream;
+ * ignored in MBOTS_EXEC_CPU mode, where every call completes before returning).
  *
  * Ownership (mgr.cpp:70-76): the handle owns every device buffer; tensors
  * returned by mbots_export are non-owning views that stay valid until the next
@@ -34,6 +35,11 @@ extern "C" {
 #define MBOTS_FLAG_REWARD_FIXED     0x1u  /* rewards[speciesID-1] (fixes sim.cpp:943) */
 #define MBOTS_FLAG_FIX_DEPTH_ALIAS  0x2u  /* depth_tensor exports real depth (sim.cpp:102-112) */
 
+/* execution modes (madrona::ExecMode; the reference's callers pick CPU when
+ * no GPU is present, learn/env.py:12-15) */
+#define MBOTS_EXEC_HIP  0   /* gfx950 kernels on device gpu_id (default)     */
+#define MBOTS_EXEC_CPU  1   /* host threads; bit-identical results, host views */
+
 /* Manager::Config (src/entry/mgr.hpp:12-23) plus sharding / capacity knobs. */
 typedef struct mbots_config {
     int32_t  gpu_id;                    /* gpuID                              */
@@ -44,6 +50,7 @@ typedef struct mbots_config {
     uint32_t world_offset;              /* global index of world 0 (shards)   */
     uint32_t agent_capacity;            /* per-world slot cap (0 -> 128)      */
     uint32_t flags;                     /* MBOTS_FLAG_*                       */
+    int32_t  exec_mode;                 /* MBOTS_EXEC_* (ExecMode)            */
 } mbots_config;
 
 /* Export slots; numbering mirrors enum class ExportID (src/sim/sim.hpp:18-55). */
@@ -84,11 +91,11 @@ enum mbots_dtype {
     MBOTS_DTYPE_FLOAT32 = 3
 };
 
-/* A non-owning 2-D device tensor view (madrona::py::Tensor, mgr.cpp:70-76). */
+/* A non-owning 2-D tensor view (madrona::py::Tensor, mgr.cpp:70-76). */
 typedef struct mbots_tensor {
     void   *data;        /* device pointer                                  */
     int32_t dtype;       /* enum mbots_dtype                                */
-    int32_t device;      /* HIP device ordinal (gpuID)                      */
+    int32_t device;      /* HIP device ordinal (gpuID); -1: host memory (CPU mode) */
     int64_t dims[2];     /* rows, columns                                   */
 } mbots_tensor;
 

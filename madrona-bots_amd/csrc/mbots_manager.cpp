@@ -14,11 +14,14 @@
 #include <hip/hip_ext.h>
 #include "../../include/mbots.h"
 #include "mbots_kernels.hpp"
+#include "mbots_cpu.hpp"
 
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
 #include <cstring>
+#include <memory>
+#include <new>
 #include <string>
 #include <vector>
 
@@ -61,6 +64,7 @@ struct TimedPair {
 
 struct mbots_handle {
     mbots_config cfg{};
+    std::unique_ptr<mbots::cpu::Sim> cpu;   // MBOTS_EXEC_CPU: the host world step
     int device = 0;
     mbots::SimState S{};
     mbots::ObsTable T[2]{};
@@ -358,6 +362,22 @@ int mbots_create(const mbots_config *cfg_in, mbots_handle **out)
         return fail(MBOTS_E_INVALID, "init_num_agents_per_world must be >= 4");
     const uint64_t rows = (uint64_t)cfg.num_worlds * cfg.agent_capacity;
     if (rows >= (1ull << 31)) return fail(MBOTS_E_INVALID, "num_worlds * agent_capacity >= 2^31");
+    if (cfg.exec_mode != MBOTS_EXEC_HIP && cfg.exec_mode != MBOTS_EXEC_CPU)
+        return fail(MBOTS_E_INVALID, "exec_mode must be MBOTS_EXEC_HIP or MBOTS_EXEC_CPU");
+    if (cfg.exec_mode == MBOTS_EXEC_CPU) {   // no HIP call on this path: runs without a GPU
+        mbots_handle *h = new (std::nothrow) mbots_handle();
+        if (!h) return fail(MBOTS_E_NOMEM, "host allocation failed");
+        h->cfg = cfg;
+        h->device = -1;
+        try {
+            h->cpu = std::make_unique<mbots::cpu::Sim>(cfg);
+        } catch (const std::bad_alloc &) {
+            delete h;
+            return fail(MBOTS_E_NOMEM, "host allocation of the CPU-mode state failed");
+        }
+        *out = h;
+        return MBOTS_OK;
+    }
 
     int ndev = 0;
     HIP_TRY(hipGetDeviceCount(&ndev));
@@ -450,6 +470,10 @@ int mbots_create(const mbots_config *cfg_in, mbots_handle **out)
 int mbots_destroy(mbots_handle *h)
 {
     if (!h) return MBOTS_OK;
+    if (h->cpu) {
+        delete h;
+        return MBOTS_OK;
+    }
     (void)hipSetDevice(h->device);
     (void)hipDeviceSynchronize();
     for (auto &p : h->pending) { (void)hipEventDestroy(p.a); (void)hipEventDestroy(p.b); }
@@ -466,6 +490,10 @@ int mbots_destroy(mbots_handle *h)
 int mbots_step(mbots_handle *h, void *stream)
 {
     if (!h) return fail(MBOTS_E_INVALID, "null handle");
+    if (h->cpu) {
+        h->cpu->step();
+        return MBOTS_OK;
+    }
     HIP_TRY(hipSetDevice(h->device));
     hipStream_t st = as_stream(stream);
     h->last_stream = st;
@@ -533,6 +561,10 @@ int mbots_step(mbots_handle *h, void *stream)
 int mbots_shift_observations(mbots_handle *h, void *stream)
 {
     if (!h) return fail(MBOTS_E_INVALID, "null handle");
+    if (h->cpu) {
+        h->cpu->shift_observations();
+        return MBOTS_OK;
+    }
     HIP_TRY(hipSetDevice(h->device));
     hipStream_t st = as_stream(stream);
     h->last_stream = st;
@@ -562,6 +594,10 @@ int mbots_shift_observations(mbots_handle *h, void *stream)
 int mbots_num_agents(mbots_handle *h, uint32_t *out)
 {
     if (!h || !out) return fail(MBOTS_E_INVALID, "null argument");
+    if (h->cpu) {
+        *out = h->cpu->num_agents();
+        return MBOTS_OK;
+    }
     int rc = sync_totals(h);
     if (rc) return rc;
     *out = h->h_totals[0];
@@ -572,6 +608,10 @@ int mbots_export(mbots_handle *h, int32_t id, mbots_tensor *out)
 {
     using namespace mbots;
     if (!h || !out) return fail(MBOTS_E_INVALID, "null argument");
+    if (h->cpu) {
+        const int r = h->cpu->export_tensor(id, out);
+        return r ? fail(r, "unknown export id " + std::to_string(id)) : MBOTS_OK;
+    }
     uint32_t N = 0;
     int rc = mbots_num_agents(h, &N);
     if (rc) return rc;
@@ -651,6 +691,10 @@ int mbots_set_action(mbots_handle *h, uint32_t row, const int32_t action[6])
     int rc = mbots_num_agents(h, &N);
     if (rc) return rc;
     if (row >= N) return fail(MBOTS_E_RANGE, "agent row out of range");
+    if (h->cpu) {
+        memcpy(&h->cpu->table().action[(size_t)row * 6], action, 6 * sizeof(int32_t));
+        return MBOTS_OK;
+    }
     if ((rc = materialize_cur_ah(h, h->last_stream))) return rc;
     HIP_TRY(hipMemcpyAsync(h->T[h->tb].action + (size_t)row * 6, action, 6 * sizeof(int32_t),
                            hipMemcpyHostToDevice, h->last_stream));
@@ -662,6 +706,10 @@ int mbots_agent_offset_for_world(mbots_handle *h, uint32_t world, uint32_t *out)
 {
     if (!h || !out) return fail(MBOTS_E_INVALID, "null argument");
     if (world >= h->cfg.num_worlds) return fail(MBOTS_E_RANGE, "world out of range");
+    if (h->cpu) {
+        *out = h->cpu->world_offset_of(world);
+        return MBOTS_OK;
+    }
     int rc = sync_totals(h);
     if (rc) return rc;
     int32_t v = 0;
@@ -674,6 +722,10 @@ int mbots_write_synthetic_actions(mbots_handle *h, uint32_t seed, uint32_t step,
                                   int32_t write_hidden, void *stream)
 {
     if (!h) return fail(MBOTS_E_INVALID, "null handle");
+    if (h->cpu) {
+        h->cpu->write_synthetic_actions(seed, step, write_hidden != 0);
+        return MBOTS_OK;
+    }
     HIP_TRY(hipSetDevice(h->device));
     hipStream_t st = as_stream(stream);
     h->last_stream = st;
@@ -688,6 +740,10 @@ int mbots_construct_obs(mbots_handle *h, int32_t prev, float *out, uint64_t out_
 {
     if (!h || !out) return fail(MBOTS_E_INVALID, "null argument");
     if (out_rows > 0xFFFFFFFFull) return fail(MBOTS_E_INVALID, "out_rows too large");
+    if (h->cpu) {
+        h->cpu->construct_obs(prev != 0, out, out_rows);
+        return MBOTS_OK;
+    }
     HIP_TRY(hipSetDevice(h->device));
     hipStream_t st = as_stream(stream);
     h->last_stream = st;
@@ -703,6 +759,10 @@ int mbots_construct_obs(mbots_handle *h, int32_t prev, float *out, uint64_t out_
 int mbots_agent_steps(mbots_handle *h, uint64_t *out)
 {
     if (!h || !out) return fail(MBOTS_E_INVALID, "null argument");
+    if (h->cpu) {
+        *out = h->cpu->agent_steps();
+        return MBOTS_OK;
+    }
     HIP_TRY(hipSetDevice(h->device));
     HIP_TRY(hipDeviceSynchronize());
     unsigned long long v = 0;
@@ -714,6 +774,10 @@ int mbots_agent_steps(mbots_handle *h, uint64_t *out)
 int mbots_overflow(mbots_handle *h, uint64_t *out)
 {
     if (!h || !out) return fail(MBOTS_E_INVALID, "null argument");
+    if (h->cpu) {
+        *out = h->cpu->overflow();
+        return MBOTS_OK;
+    }
     HIP_TRY(hipSetDevice(h->device));
     HIP_TRY(hipDeviceSynchronize());
     std::vector<uint32_t> v(h->cfg.num_worlds);
@@ -732,6 +796,10 @@ int mbots_overflow(mbots_handle *h, uint64_t *out)
 int mbots_checkpoint_size(mbots_handle *h, uint64_t *out)
 {
     if (!h || !out) return fail(MBOTS_E_INVALID, "null argument");
+    if (h->cpu) {
+        *out = h->cpu->checkpoint_bytes();
+        return MBOTS_OK;
+    }
     int rc = sync_totals(h);
     if (rc) return rc;
     *out = ckpt_bytes(ckpt_segments(h, h->T[h->tb], h->h_totals[0]));
@@ -741,6 +809,11 @@ int mbots_checkpoint_size(mbots_handle *h, uint64_t *out)
 int mbots_save_checkpoint(mbots_handle *h, void *dst, uint64_t bytes)
 {
     if (!h || !dst) return fail(MBOTS_E_INVALID, "null argument");
+    if (h->cpu) {
+        std::string err;
+        const int r = h->cpu->save(dst, bytes, err);
+        return r ? fail(r, err) : MBOTS_OK;
+    }
     HIP_TRY(hipSetDevice(h->device));
     int rc0 = materialize_prev(h, h->last_stream);
     if (!rc0) rc0 = materialize_prev_ah(h, h->last_stream);
@@ -778,6 +851,11 @@ int mbots_save_checkpoint(mbots_handle *h, void *dst, uint64_t bytes)
 int mbots_load_checkpoint(mbots_handle *h, const void *src, uint64_t bytes)
 {
     if (!h || !src) return fail(MBOTS_E_INVALID, "null argument");
+    if (h->cpu) {
+        std::string err;
+        const int r = h->cpu->load(src, bytes, err);
+        return r ? fail(r, err) : MBOTS_OK;
+    }
     if (bytes < sizeof(CkptHeader)) return fail(MBOTS_E_INVALID, "checkpoint truncated");
     CkptHeader hd;
     memcpy(&hd, src, sizeof(hd));
@@ -822,6 +900,10 @@ int mbots_world_state(mbots_handle *h, uint32_t world, float *xy_rwrz, int32_t *
     using namespace mbots;
     if (!h || !xy_rwrz || !sp_hp_finder || !food || !n_out) return fail(MBOTS_E_INVALID, "null argument");
     if (world >= h->cfg.num_worlds) return fail(MBOTS_E_INVALID, "world out of range");
+    if (h->cpu) {
+        h->cpu->world_state(world, xy_rwrz, sp_hp_finder, food, food_rot, n_out);
+        return MBOTS_OK;
+    }
     HIP_TRY(hipSetDevice(h->device));
     HIP_TRY(hipDeviceSynchronize());
     const SimState &S = h->S;
@@ -848,6 +930,7 @@ int mbots_world_state(mbots_handle *h, uint32_t world, float *xy_rwrz, int32_t *
 int mbots_enable_kernel_timing(mbots_handle *h, int32_t enable)
 {
     if (!h) return fail(MBOTS_E_INVALID, "null handle");
+    if (h->cpu) return MBOTS_OK;   // no kernels
     HIP_TRY(hipSetDevice(h->device));
     HIP_TRY(hipDeviceSynchronize());
     for (auto &p : h->pending) { h->pool.push_back(p.a); h->pool.push_back(p.b); }
@@ -860,6 +943,13 @@ int mbots_enable_kernel_timing(mbots_handle *h, int32_t enable)
 int mbots_kernel_times(mbots_handle *h, double ms[MBOTS_TK_COUNT], uint64_t launches[MBOTS_TK_COUNT])
 {
     if (!h) return fail(MBOTS_E_INVALID, "null handle");
+    if (h->cpu) {
+        for (int k = 0; k < MBOTS_TK_COUNT; ++k) {
+            if (ms) ms[k] = 0.0;
+            if (launches) launches[k] = 0;
+        }
+        return MBOTS_OK;
+    }
     HIP_TRY(hipSetDevice(h->device));
     for (auto &p : h->pending) {
         HIP_TRY(hipEventSynchronize(p.b));

@@ -6,10 +6,12 @@ learn/training_loop.py:29-137 without the learner math (out of scope):
     (learn/util.py:14-29) -> sample actions -> shift_observations() ->
     write one-hot actions into action_tensor rows (env.py:94-98).
 
-Works with anything exposing the SimManager surface (madrona_bots.SimManager
-on a GPU; tests/oracle_adapter.py on the CPU for BASELINE config 1).
+Works with anything exposing the SimManager surface: madrona_bots.SimManager
+with exec_mode "hip" (a GPU) or "cpu" (BASELINE config 1: 64 worlds without a
+GPU; like learn/env.py:12-15 the default picks cpu when no GPU is present).
 
     python madrona-bots_amd/harness/rollout.py --worlds 4096 --steps 100
+    python madrona-bots_amd/harness/rollout.py --worlds 64 --exec-mode cpu
 """
 import argparse
 import json
@@ -94,15 +96,18 @@ def main():
     ap.add_argument("--seed", type=int, default=69)
     ap.add_argument("--agents", type=int, default=32)
     ap.add_argument("--fused", action="store_true", help="sim.construct_obs instead of torch.cat")
+    ap.add_argument("--exec-mode", default="auto", choices=("auto", "hip", "cpu"),
+                    help="auto: hip when a GPU is present, else cpu (learn/env.py:12-15)")
     a = ap.parse_args()
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     import madrona_bots as mb
-    dev = torch.device("cuda", 0)
-    sim = mb.SimManager(0, a.worlds, a.seed, a.agents)
+    mode = a.exec_mode if a.exec_mode != "auto" else ("hip" if torch.cuda.is_available() else "cpu")
+    dev = torch.device("cuda", 0) if mode == "hip" else torch.device("cpu")
+    sim = mb.SimManager(0, a.worlds, a.seed, a.agents, exec_mode=mode)
     random_rollout(sim, 5, device=dev, fused=a.fused)
     st = random_rollout(sim, a.steps, device=dev, fused=a.fused)
     # the reference's "Average FPS for simulator" = num_worlds / mean step time
-    print(json.dumps({"worlds": a.worlds, "steps": st["steps"],
+    print(json.dumps({"worlds": a.worlds, "exec_mode": mode, "steps": st["steps"],
                       "world_steps_per_s": a.worlds * st["steps"] / st["step_s"],
                       "agent_steps_per_s_step_only": st["agent_steps"] / st["step_s"]}))
 

@@ -10,10 +10,13 @@ Mirrors the nanobind surface of src/entry/entry.cpp:16-45:
         .stats_tensor(is_prev)  .hidden_state_tensor(is_prev)
 
 Each accessor returns a ``Tensor`` whose ``to_torch()`` is a zero-copy torch
-view of device memory owned by the manager (madrona::py::Tensor,
-mgr.cpp:70-76).  The simulation runs in libmbots.so (hand-written gfx950
-kernels); there is no CPU fallback -- importing without the built library
-raises ImportError.
+view of memory owned by the manager (madrona::py::Tensor, mgr.cpp:70-76).
+The simulation runs in libmbots.so: hand-written gfx950 kernels
+(``exec_mode="hip"``, the default) or, for ``exec_mode="cpu"``
+(madrona::ExecMode::CPU; learn/env.py:12-15 picks it without a GPU), the same
+world step on host threads with bit-identical results and host tensor views.
+Importing without the built library raises ImportError; a HIP-mode manager
+without a GPU raises RuntimeError (no silent fallback).
 """
 import ctypes
 import os
@@ -21,7 +24,7 @@ import types
 
 import torch  # loads the HIP runtime libmbots.so links against (same soname)
 
-__all__ = ["SimManager", "Tensor", "madrona", "ExportID"]
+__all__ = ["SimManager", "Tensor", "madrona", "ExportID", "ExecMode"]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # MBOTS_LIB: developer override to A/B alternative builds of the same library
@@ -37,7 +40,8 @@ class _Config(ctypes.Structure):
     _fields_ = [("gpu_id", ctypes.c_int32), ("num_worlds", ctypes.c_uint32),
                 ("rand_seed", ctypes.c_uint32), ("init_num_agents_per_world", ctypes.c_uint32),
                 ("sensor_size", ctypes.c_uint32), ("world_offset", ctypes.c_uint32),
-                ("agent_capacity", ctypes.c_uint32), ("flags", ctypes.c_uint32)]
+                ("agent_capacity", ctypes.c_uint32), ("flags", ctypes.c_uint32),
+                ("exec_mode", ctypes.c_int32)]
 
 
 class _CTensor(ctypes.Structure):
@@ -102,6 +106,24 @@ _DTYPES = {0: (torch.uint8, "|u1"), 1: (torch.int8, "|i1"), 2: (torch.int32, "<i
 FLAG_REWARD_FIXED = 0x1
 FLAG_FIX_DEPTH_ALIAS = 0x2
 
+
+class ExecMode:
+    """madrona::ExecMode (MBOTS_EXEC_*)."""
+    CUDA = HIP = 0
+    CPU = 1
+
+
+def _exec_mode(v):
+    if isinstance(v, str):
+        v = {"hip": ExecMode.HIP, "cuda": ExecMode.HIP, "gpu": ExecMode.HIP,
+             "cpu": ExecMode.CPU}.get(v.lower())
+        if v is None:
+            raise ValueError("exec_mode must be 'hip' or 'cpu'")
+    v = int(v)
+    if v not in (ExecMode.HIP, ExecMode.CPU):
+        raise ValueError(f"unknown exec_mode {v}")
+    return v
+
 # TK_* indices of mbots_kernel_times
 OBS_DIM = 69   # learn/env.py:19
 KERNELS = ("world_step", "scan", "export", "sensor", "shift", "actions", "move")
@@ -130,7 +152,9 @@ class Tensor:
                 "version": 3, "strides": None, "stream": None}
 
     def to_torch(self):
-        """Zero-copy torch view on cuda:<gpu_id>."""
+        """Zero-copy torch view on cuda:<gpu_id> (host memory in CPU mode)."""
+        if self._device < 0:
+            return self._host_view()
         dev = torch.device("cuda", self._device)
         if self.shape[0] == 0:
             return torch.empty(self.shape, dtype=self._torch_dtype, device=dev)
@@ -140,21 +164,38 @@ class Tensor:
         return t
 
 
+    def _host_view(self):
+        import numpy as np
+        npdt = {torch.uint8: np.uint8, torch.int8: np.int8, torch.int32: np.int32,
+                torch.float32: np.float32}[self._torch_dtype]
+        n = self.shape[0] * self.shape[1]
+        if n == 0:
+            return torch.empty(self.shape, dtype=self._torch_dtype)
+        buf = (ctypes.c_char * (n * np.dtype(npdt).itemsize)).from_address(self._ptr)
+        t = torch.from_numpy(np.frombuffer(buf, dtype=npdt, count=n).reshape(self.shape))
+        if t.data_ptr() != self._ptr:
+            raise RuntimeError("madrona_bots: to_torch() produced a copy, expected a view")
+        return t
+
+
 madrona = types.ModuleType("madrona_bots.madrona")
+madrona.ExecMode = ExecMode
 madrona.Tensor = Tensor
 
 
 class SimManager:
     """Manager (src/entry/mgr.hpp:10-68) with the nanobind constructor
-    signature (entry.cpp:17-28).  Keyword-only extensions: agent_capacity
+    signature (entry.cpp:17-28).  Keyword-only extensions: exec_mode ("hip" /
+    "cpu" or ExecMode.*: the Manager's ExecMode), agent_capacity
     (per-world slot cap), world_offset (global index of this shard's first
     world), reward_fixed (rewards[speciesID-1] instead of the reference's
     off-by-one), fix_depth_alias (depth_tensor returns real depth,
     SURVEY B.1)."""
 
     def __init__(self, gpu_id, num_worlds, rand_seed, init_num_agents_per_world, *,
-                 agent_capacity=128, world_offset=0, reward_fixed=False,
+                 exec_mode="hip", agent_capacity=128, world_offset=0, reward_fixed=False,
                  fix_depth_alias=False):
+        self.exec_mode = _exec_mode(exec_mode)
         self.gpu_id = int(gpu_id)
         self.num_worlds = int(num_worlds)
         self.agent_capacity = int(agent_capacity)
@@ -162,7 +203,7 @@ class SimManager:
                 (FLAG_FIX_DEPTH_ALIAS if fix_depth_alias else 0)
         cfg = _Config(self.gpu_id, self.num_worlds, int(rand_seed) & 0xFFFFFFFF,
                       int(init_num_agents_per_world), 32, int(world_offset),
-                      int(agent_capacity), flags)
+                      int(agent_capacity), flags, self.exec_mode)
         h = ctypes.c_void_p()
         _check(_lib.mbots_create(ctypes.byref(cfg), ctypes.byref(h)))
         self._h = h
@@ -174,7 +215,16 @@ class SimManager:
             self._h = None
 
     def _stream(self):
+        if self.exec_mode == ExecMode.CPU:
+            return ctypes.c_void_p(None)
         return ctypes.c_void_p(torch.cuda.current_stream(self.gpu_id).cuda_stream)
+
+    @property
+    def device(self):
+        """torch device of the exported views."""
+        if self.exec_mode == ExecMode.CPU:
+            return torch.device("cpu")
+        return torch.device("cuda", self.gpu_id)
 
     # -- graphs -------------------------------------------------------------
     def step(self):
@@ -252,11 +302,11 @@ class SimManager:
         import torch
         n = self.num_agents()
         if out is None:
-            out = torch.empty((n, OBS_DIM), dtype=torch.float32,
-                              device=torch.device("cuda", self.gpu_id))
-        if out.dtype != torch.float32 or not out.is_cuda or not out.is_contiguous() \
+            out = torch.empty((n, OBS_DIM), dtype=torch.float32, device=self.device)
+        if out.dtype != torch.float32 or out.device != self.device or not out.is_contiguous() \
                 or out.dim() != 2 or out.shape[1] != OBS_DIM or out.shape[0] < n:
-            raise ValueError(f"out must be a contiguous CUDA float32 [>= {n}, {OBS_DIM}] tensor")
+            raise ValueError(f"out must be a contiguous float32 [>= {n}, {OBS_DIM}] tensor on "
+                             f"{self.device}")
         _check(_lib.mbots_construct_obs(self._h, 1 if is_prev else 0,
                                         ctypes.c_void_p(out.data_ptr()), out.shape[0],
                                         self._stream()))

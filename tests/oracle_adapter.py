@@ -1,7 +1,7 @@
 """TEST INFRASTRUCTURE: the CPU oracle behind the SimManager surface, with
-zero-copy CPU torch views -- lets the rollout harness run BASELINE config 1
-(64 worlds, CPU, "plumbing, runs without a GPU") in the CPU suite.  Not a
-product path: madrona_bots has no CPU mode."""
+zero-copy CPU torch views -- the checker the rollout harness's config-1 run
+through the product's own CPU execution mode (madrona_bots.SimManager(...,
+exec_mode="cpu")) is compared with.  Not a product path."""
 import numpy as np
 import torch
 

@@ -1,0 +1,153 @@
+"""CPU execution mode (exec_mode="cpu", the reference Manager's ExecMode::CPU;
+BASELINE config 1: "64 worlds, ExecMode::CPU via learn/env.py, runs without a
+GPU").  The product's host path (madrona-bots_amd/csrc/mbots_cpu.cpp, inside
+libmbots.so) against the oracle, bitwise on every exported column -- no GPU
+needed, so these run in the CPU suite."""
+import numpy as np
+import pytest
+import torch
+
+import pyoracle
+from simpair import compare
+
+
+def _mgr(W, seed=69, A=32, **kw):
+    import madrona_bots as mb
+    return mb.SimManager(0, W, seed, A, exec_mode="cpu", **kw)
+
+
+def _pair(W, seed=69, A=32, steps=10, cap=128, reward_fixed=False, depth_fixed=False,
+          world_offset=0, write_hidden=True):
+    mgr = _mgr(W, seed, A, agent_capacity=cap, reward_fixed=reward_fixed,
+               fix_depth_alias=depth_fixed, world_offset=world_offset)
+    orc = pyoracle.OracleSim(W, seed, A, cap=cap, reward_fixed=reward_fixed,
+                             world_offset=world_offset, num_threads=4)
+    errs = compare(mgr, orc, "init", depth_fixed=depth_fixed)
+    assert not errs, errs[:5]
+    for t in range(steps):
+        mgr.write_synthetic_actions(1234, t, write_hidden)
+        orc.write_synthetic_actions(1234, t, write_hidden)
+        mgr.step()
+        orc.step()
+        errs = compare(mgr, orc, f"step {t}", depth_fixed=depth_fixed)
+        assert not errs, errs[:5]
+        mgr.shift_observations()
+        orc.shift_observations()
+        errs = compare(mgr, orc, f"shift {t}", depth_fixed=depth_fixed)
+        assert not errs, errs[:5]
+    return mgr, orc
+
+
+def test_config1_64_worlds_matches_oracle():
+    _pair(64, steps=25)
+
+
+def test_reward_fixed_depth_seed_offset():
+    _pair(16, seed=7, steps=12, reward_fixed=True, depth_fixed=True, world_offset=1000)
+
+
+def test_small_population_and_capacity_overflow():
+    mgr, orc = _pair(32, A=4, steps=20, cap=8)
+    assert mgr.overflow() == orc.overflow()
+
+
+def test_views_are_host_zero_copy_and_writable():
+    mgr = _mgr(8)
+    mgr.step()
+    n = mgr.num_agents()
+    a = mgr.action_tensor(False).to_torch()
+    assert a.device.type == "cpu" and tuple(a.shape) == (n, 6) and a.dtype == torch.int32
+    a.zero_()
+    a[3, 5] = 1
+    assert int(mgr.action_tensor(False).to_torch()[3, 5]) == 1
+    mgr.set_action(4, 1, 0, 0, 0, 0, 0)
+    assert mgr.action_tensor(False).to_torch()[4].tolist() == [1, 0, 0, 0, 0, 0]
+    h = mgr.health_tensor(False).to_torch()
+    assert h.dtype == torch.float32 and int(h.view(torch.int32).max()) <= 200
+    assert tuple(mgr.species_count_tensor().to_torch().shape) == (8, 4)
+    assert tuple(mgr.done_tensor().to_torch().shape) == (n, 1)
+
+
+def test_offsets_sensor_index_and_world_state():
+    mgr, orc = _pair(24, steps=6)
+    counts, offsets = orc.world_counts()
+    assert [mgr.agent_offset_for_world(w) for w in range(24)] == offsets.tolist()
+    si = mgr.sensor_index_tensor().to_torch().numpy().ravel()
+    assert np.array_equal(si, orc.sensor_index())
+    for w in (0, 11, 23):
+        g, o = mgr.world_state(w), orc.world_state(w)
+        assert np.array_equal(g["position"].view(np.int32), o["xy"].view(np.int32))
+        assert np.array_equal(g["finder"], o["finder"])
+        assert np.array_equal(g["food"], o["food"])
+
+
+def test_construct_obs_matches_torch_cat():
+    mgr, _ = _pair(8, steps=3)
+    for prev in (False, True):
+        want = torch.cat((mgr.depth_tensor(prev).to_torch(), mgr.health_tensor(prev).to_torch(),
+                          mgr.position_tensor(prev).to_torch(), mgr.semantic_tensor(prev).to_torch(),
+                          mgr.surrounding_tensor(prev).to_torch()), dim=1)
+        got = mgr.construct_obs(prev)
+        assert got.device.type == "cpu"
+        assert torch.equal(got.view(torch.int32), want.view(torch.int32))
+
+
+def test_checkpoint_continues_bit_exactly(tmp_path):
+    a = _mgr(16)
+    for t in range(5):
+        a.write_synthetic_actions(1234, t, True)
+        a.step()
+        a.shift_observations()
+    blob = a.save_checkpoint(tmp_path / "ck.bin")
+    b = _mgr(16)
+    b.load_checkpoint(tmp_path / "ck.bin")
+    for t in range(5, 9):
+        for m in (a, b):
+            m.write_synthetic_actions(1234, t, True)
+            m.step()
+            m.shift_observations()
+    for name in ("position_tensor", "reward_tensor", "semantic_tensor", "hidden_state_tensor"):
+        for prev in (False, True):
+            assert torch.equal(getattr(a, name)(prev).to_torch(), getattr(b, name)(prev).to_torch())
+    with pytest.raises(RuntimeError):
+        _mgr(8).load_checkpoint(blob.tobytes())
+
+
+def test_bad_exec_mode_rejected():
+    import madrona_bots as mb
+    with pytest.raises(ValueError):
+        mb.SimManager(0, 4, 69, 32, exec_mode="tpu")
+
+
+@pytest.mark.gpu
+def test_cpu_mode_equals_hip_mode():
+    """The two execution modes of one library: the same stream leaves the same
+    bits in every column (config 1 size)."""
+    g = _pair_modes(64, steps=12)
+    assert g
+
+
+def _pair_modes(W, steps):
+    import madrona_bots as mb
+    h = mb.SimManager(0, W, 69, 32)
+    c = _mgr(W)
+    for t in range(steps):
+        for m in (h, c):
+            m.write_synthetic_actions(1234, t, True)
+            m.step()
+        _same(h, c, f"step {t}")
+        for m in (h, c):
+            m.shift_observations()
+        _same(h, c, f"shift {t}")
+    return True
+
+
+def _same(h, c, where):
+    assert h.num_agents() == c.num_agents(), where
+    for name in ("species_tensor", "position_tensor", "health_tensor", "surrounding_tensor",
+                 "reward_tensor", "action_tensor", "stats_tensor", "hidden_state_tensor",
+                 "semantic_tensor", "depth_tensor"):
+        for prev in (False, True):
+            a = getattr(h, name)(prev).to_torch().cpu()
+            b = getattr(c, name)(prev).to_torch()
+            assert torch.equal(a.view(torch.uint8), b.view(torch.uint8)), (where, name, prev)

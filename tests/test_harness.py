@@ -1,6 +1,7 @@
 """The rollout harness (madrona-bots_amd/harness/rollout.py, the learn/env.py
-call sequence): BASELINE config 1 -- 64 worlds on the CPU through the oracle
-adapter -- and the same loop on the GPU product."""
+call sequence): BASELINE config 1 -- 64 worlds through the product's CPU
+execution mode, checked against the same loop over the oracle adapter -- and
+the same loop on the GPU product."""
 import os
 import sys
 
@@ -16,19 +17,32 @@ from oracle_adapter import OracleSimManager  # noqa: E402
 
 @pytest.mark.parametrize("per_species", [False, True])
 def test_config1_cpu_rollout(per_species):
-    sim = OracleSimManager(0, 64, 69, 32)
+    """BASELINE config 1: 64 worlds, exec_mode="cpu", no GPU; the rollout (the
+    learner's torch.randint actions written through the views) leaves exactly
+    the oracle's tables."""
+    import madrona_bots as mb
+    sim = mb.SimManager(0, 64, 69, 32, exec_mode="cpu")
+    ref = OracleSimManager(0, 64, 69, 32)
     st = rollout.random_rollout(sim, 8, shift_per_species=per_species)
+    rollout.random_rollout(ref, 8, shift_per_species=per_species)
     assert st["steps"] == 8 and st["agent_steps"] >= 64 * 32 * 8
     offs = rollout.species_offsets(sim)
+    assert offs == rollout.species_offsets(ref)
     assert offs[0][0] == 0 and all(a[1] == b[0] for a, b in zip(offs, offs[1:]))
     obs = rollout.construct_obs(sim, *offs[2])
     assert obs.shape[1] == rollout.OBS_DIM == 69 and obs.dtype == torch.float32
+    for name in ("position_tensor", "reward_tensor", "semantic_tensor", "action_tensor",
+                 "hidden_state_tensor", "stats_tensor"):
+        for prev in (False, True):
+            a, b = getattr(sim, name)(prev).to_torch(), getattr(ref, name)(prev).to_torch()
+            assert torch.equal(a.view(torch.uint8), b.view(torch.uint8)), (name, prev)
 
 
 def test_per_species_shift_overwrites_prev_actions():
     # SURVEY B.9: shifting inside the species loop makes PrevAction of species
     # 1..3 equal their *new* actions; only species 4 keeps its true previous ones
-    sim = OracleSimManager(0, 8, 69, 32)
+    import madrona_bots as mb
+    sim = mb.SimManager(0, 8, 69, 32, exec_mode="cpu")
     rollout.random_rollout(sim, 3, shift_per_species=True)
     offs = rollout.species_offsets(sim)
     act = sim.action_tensor(False).to_torch()
