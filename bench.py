@@ -14,8 +14,15 @@ BASELINE config 3).  Rank 0 prints one JSON line.
 --gather (BASELINE config 5): every step also builds the learner observation
 rows (fused construct_obs kernel) and gathers them with the rewards to rank 0
 over RCCL (madrona-bots_amd/harness/gather.py); reported as "config5".
-A secondary line at 4096 worlds/GPU (BASELINE config 2; the metric names both
-sizes) is measured after the main one unless --no-secondary.
+
+After the main line (unless --no-secondary): the reference training loop's
+call sequence (learn/training_loop.py:36-137 without the learner math: step,
+the action / memory views, reward and health clones, construct_obs of the
+current and previous rows, PrevHiddenState, shift, the learner's one-hot
+actions and memory written back) at 4096 worlds/GPU -- BASELINE config 2,
+"random-action rollout, obs/reward tensors on-device", reported as
+"secondary" -- and at the main line's size ("reference_loop"), each with its
+own HBM roofline.
 """
 import argparse
 import json
@@ -42,6 +49,28 @@ AGENTS_PER_WORLD = 32       # learn/env.py:15
 def algorithmic_bytes(n_agents, n_worlds):
     """B_step = 552 N + 1952 W bytes per step (step + shift)."""
     return 552.0 * n_agents + 1952.0 * n_worlds
+
+
+# B_step counts 88 B per agent the lazy shift never moves when nothing reads
+# the table between step() and shift_observations() (the 44 B of previous-obs
+# reads and the 44 B of Prev{Species,Position,Health,Surrounding,Reward,Stats}
+# writes, DESIGN.md "Lazy shift"): the bytes the bench loop must move
+LAZY_BYTES_PER_AGENT = 552.0 - 88.0
+# the reference loop on top of B_step: construct_obs of the current and the
+# previous rows (84 B read + 276 B written each), the reward / health clones
+# (4 + 4 B each way), the learner's one-hot action + memory write (24 + 64 B)
+LOOP_EXTRA_PER_AGENT = 2 * (84.0 + 276.0) + 16.0 + 88.0
+
+
+def cpu_share():
+    """Host CPUs this process may use: its affinity set, capped by the box's
+    per-GPU share (OMP_NUM_THREADS, 16 on the GPU box); and the machine's."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count() or 1
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return (min(aff, omp) if omp > 0 else aff), aff, os.cpu_count()
 
 
 def load_traffic(worlds):
@@ -93,37 +122,59 @@ def load_profile(suffix, worlds):
 
 
 def cpu_baseline(worlds_sample, target_s):
-    """The C oracle (oracle/, test infrastructure) on host cores: a bounded
-    sample of the same workload (same seed/actions), world-parallel threads."""
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import pyoracle
-    threads = max(1, min(16, os.cpu_count() or 1))
-    sim = pyoracle.OracleSim(worlds_sample, SEED, AGENTS_PER_WORLD, cap=128, num_threads=threads)
-    agent_steps, steps = 0, 0
+    """The build's C++ CPU restatement (SURVEY 8d "CPU baseline"): the
+    product's own CPU execution mode (madrona_bots exec_mode="cpu",
+    mbots_cpu.cpp: the same systems, bit-identical to the HIP path), worlds
+    split over every host thread this process is given, on a bounded sample
+    of the same workload (same seed, agents, action stream, step+shift+write)."""
+    import madrona_bots as mb
+    threads, aff, nproc = cpu_share()
+    os.environ["MBOTS_CPU_THREADS"] = str(threads)
+    sim = mb.SimManager(0, worlds_sample, SEED, AGENTS_PER_WORLD, exec_mode="cpu")
+    sim.write_synthetic_actions(ACTION_SEED, 0)
+    sim.step()
+    sim.shift_observations()
+    s0, steps = sim.agent_steps(), 0
     t0 = time.perf_counter()
     while True:
-        sim.write_synthetic_actions(ACTION_SEED, steps)
+        sim.write_synthetic_actions(ACTION_SEED, steps + 1)
         sim.step()
         sim.shift_observations()
-        agent_steps += sim.num_agents()
         steps += 1
         dt = time.perf_counter() - t0
-        if dt >= target_s or steps >= 2000:
+        if dt >= target_s or steps >= 5000:
             break
-    return {"value": agent_steps / dt, "unit": "agent-steps/s", "cores": threads,
-            "kind": "port",
+    return {"value": (sim.agent_steps() - s0) / dt, "unit": "agent-steps/s", "cores": threads,
+            "nproc": nproc, "affinity_cpus": aff, "kind": "port",
+            "impl": "madrona_bots exec_mode='cpu' (madrona-bots_amd/csrc/mbots_cpu.cpp), "
+                    "std::thread per world range",
             "sample": f"{worlds_sample} worlds x {AGENTS_PER_WORLD} agents, {steps} steps "
-                      f"(step+shift+actions), oracle/mbots_oracle.c on {threads} threads, "
-                      f"{dt:.1f} s"}
+                      f"(step+shift+actions), {threads} threads, {dt:.1f} s"}
 
 
-def secondary_run(W, args, rank, world_size, dev, distributed):
-    """BASELINE config 2 size (4096 worlds/GPU), same step, same timing rule."""
+def reference_loop(W, args, rank, world_size, dev, distributed, label):
+    """learn/training_loop.py:36-137 without the learner math (out of scope),
+    one rank's shard of W worlds; returns the line's dict."""
     import madrona_bots as mb
     m = mb.SimManager(dev.index, W, SEED, AGENTS_PER_WORLD, world_offset=rank * W)
-    m.write_synthetic_actions(ACTION_SEED, 0)
+
+    def one(t):
+        m.step()                                             # :36
+        ends = m.species_count_tensor().to_torch().sum(dim=0).cumsum(dim=0)   # :42-44
+        m.action_tensor(False).to_torch()                    # :47-48, views before the shift
+        m.hidden_state_tensor(False).to_torch()
+        rew = m.reward_tensor(False).to_torch().clone()      # :49-50
+        hp = m.health_tensor(False).to_torch().clone()
+        obs = m.construct_obs(False)                         # util.construct_obs, every species
+        prev = m.construct_obs(True)                         # :86
+        ph = m.hidden_state_tensor(True).to_torch()          # :88
+        m.shift_observations()                               # :135
+        m.write_synthetic_actions(ACTION_SEED, t + 1, True)  # :136-137 actions + memory
+        return ends, rew, hp, obs, prev, ph
+
+    m.write_synthetic_actions(ACTION_SEED, 0, True)
     for t in range(args.warmup):
-        m.step(); m.shift_observations(); m.write_synthetic_actions(ACTION_SEED, t + 1)
+        one(t)
     torch.cuda.synchronize()
     s0 = m.agent_steps()
     if distributed:
@@ -131,10 +182,11 @@ def secondary_run(W, args, rank, world_size, dev, distributed):
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for t in range(args.warmup, args.warmup + args.steps):
-        m.step(); m.shift_observations(); m.write_synthetic_actions(ACTION_SEED, t + 1)
+        one(t)
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
-    st = torch.tensor([el, float(m.agent_steps() - s0)], dtype=torch.float64,
+    n_local = m.agent_steps() - s0
+    st = torch.tensor([el, float(n_local)], dtype=torch.float64,
                       device=dev if args.backend == "nccl" else "cpu")
     if distributed:
         dist.barrier()
@@ -143,10 +195,30 @@ def secondary_run(W, args, rank, world_size, dev, distributed):
         el, total = float(tm.item()), float(tot.item())
     else:
         total = float(st[1].item())
+    ktimes = {}
+    if not args.no_kernel_timing:
+        m.enable_kernel_timing(True)
+        t = args.warmup + args.steps
+        for k in range(min(args.steps, 30)):
+            one(t + k)
+        torch.cuda.synchronize()
+        ktimes = {k: round(ms / n, 5) for k, (ms, n) in m.kernel_times().items() if n}
+        m.enable_kernel_timing(False)
     del m
+    n_mean = n_local / args.steps
+    ms = el / args.steps * 1e3
+    nb = algorithmic_bytes(n_mean, W) + LOOP_EXTRA_PER_AGENT * n_mean
+    gbs = nb / (ms * 1e-3) / 1e9
     return {"worlds_per_gpu": W, "value": total / el, "unit": "agent-steps/s",
-            "ms_per_step": el / args.steps * 1e3, "n_gpus": world_size,
-            "note": "BASELINE config 2 size, same step/timing as the main line"}
+            "ms_per_step": ms, "n_gpus": world_size, "what": label,
+            "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": gbs / HBM_PEAK_GBS, "algorithmic_bytes_per_step": nb,
+                         "bytes": "552 N + 1952 W (SURVEY 8d) + 824 N: construct_obs cur/prev "
+                                  "(84 B read + 276 B written each), reward/health clones, "
+                                  "the learner's action + memory write",
+                         "timing": "wall clock of the timed steps (host-synchronising accessors "
+                                   "included, as in the reference loop)"},
+            "kernel_ms": ktimes}
 
 
 def main():
@@ -155,7 +227,7 @@ def main():
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--worlds", type=int, default=65536, help="worlds per GPU")
-    ap.add_argument("--cpu-worlds", type=int, default=1024)
+    ap.add_argument("--cpu-worlds", type=int, default=4096)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true",
@@ -171,7 +243,7 @@ def main():
     ap.add_argument("--same-device", action="store_true",
                     help="rehearsal: every rank uses cuda:0 (with --backend gloo)")
     ap.add_argument("--no-secondary", action="store_true",
-                    help="skip the 4096-worlds/GPU secondary measurement")
+                    help="skip the reference-loop lines (config 2 at 4096 worlds/GPU, and at --worlds)")
     args = ap.parse_args()
 
     world_size = int(os.environ.get("WORLD_SIZE", "1"))
@@ -257,9 +329,13 @@ def main():
         torch.cuda.synchronize()
         ktimes = mgr.kernel_times()
         mgr.enable_kernel_timing(False)
-    secondary = None
-    if not args.no_secondary and W != 4096:
-        secondary = secondary_run(4096, args, rank, world_size, dev, distributed)
+    secondary = ref_main = None
+    if not args.no_secondary:
+        secondary = reference_loop(4096, args, rank, world_size, dev, distributed,
+                                   "BASELINE config 2: random-action rollout, obs/reward tensors "
+                                   "on device (learn/training_loop.py call sequence)")
+        ref_main = reference_loop(W, args, rank, world_size, dev, distributed,
+                                  "the reference training loop's call sequence at the main line's size")
     stats = torch.tensor([elapsed, float(agent_steps)], dtype=torch.float64,
                          device=dev if args.backend == "nccl" else "cpu")
     if distributed:
@@ -304,6 +380,17 @@ def main():
                 "algorithmic_bytes_per_launch": nb, "avg_launch_ms": span_ms,
                 "timing": f"HIP events on the launch stream around every {max(1, args.span_every)}"
                           "th step()+shift() of the timed region"}
+        # the same span priced at the bytes this design must move in this loop
+        nb_lazy = LAZY_BYTES_PER_AGENT * mean_agents + 1952.0 * W
+        lazy_gbs = nb_lazy / (span_ms * 1e-3) / 1e9
+        roof["lazy_bytes"] = {"bytes_per_agent": LAZY_BYTES_PER_AGENT, "bytes_per_step": nb_lazy,
+                              "achieved": lazy_gbs, "frac": lazy_gbs / HBM_PEAK_GBS,
+                              "note": "B_step minus the 88 B/agent of Prev* traffic the lazy shift "
+                                      "skips when nothing reads the table between step and shift"}
+        wall_gbs = nb / (elapsed / args.steps) / 1e9
+        roof["wall_clock"] = {"achieved": wall_gbs, "frac": wall_gbs / HBM_PEAK_GBS,
+                              "frac_lazy_bytes": nb_lazy / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBS,
+                              "note": "B_step / ms_per_step (includes the action write)"}
         tr = load_traffic(W)
         if tr:
             roof["traffic"] = tr[1]["bytes_per_step"]
@@ -354,6 +441,7 @@ def main():
                               "gathered_bytes_per_step": total_agent_steps / args.steps * 70 * 4}
         if secondary:
             out["secondary"] = secondary
+            out["reference_loop"] = ref_main
         if not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args.cpu_worlds, args.cpu_seconds)
         print(json.dumps(out), flush=True)

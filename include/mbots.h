@@ -163,7 +163,7 @@ int mbots_overflow(mbots_handle *h, uint64_t *out);
 enum mbots_timed_kernel {
     MBOTS_TK_WORLD_STEP = 0, MBOTS_TK_SCAN = 1, MBOTS_TK_EXPORT = 2,
     MBOTS_TK_SENSOR = 3, MBOTS_TK_SHIFT = 4, MBOTS_TK_ACTIONS = 5, MBOTS_TK_MOVE = 6,
-    MBOTS_TK_COUNT = 7
+    MBOTS_TK_OBS = 7, MBOTS_TK_COUNT = 8
 };
 int mbots_enable_kernel_timing(mbots_handle *h, int32_t enable);
 int mbots_kernel_times(mbots_handle *h, double ms[MBOTS_TK_COUNT],

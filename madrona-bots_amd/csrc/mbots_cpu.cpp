@@ -522,10 +522,12 @@ void Sim::write_synthetic_actions(uint32_t seed, uint32_t step, bool write_hidde
             const size_t r = (size_t)obsrow_[base + i];
             const uint32_t k = threefry2x32(seed, step, gw, (uint32_t)i).x % 6u;
             for (uint32_t j = 0; j < 6; ++j) t.action[r * 6 + j] = j == k ? 1 : 0;
-            if (write_hidden)
-                for (int j = 0; j < kHidden; ++j)
-                    t.hidden[r * kHidden + j] =
-                        u01(threefry2x32(seed ^ 0x9E3779B9u, step, gw, (uint32_t)i * kHidden + (uint32_t)j).x) - 0.5f;
+            if (write_hidden)   // both words of each draw: hidden[2k], hidden[2k + 1]
+                for (int q = 0; q < kHidden / 2; ++q) {
+                    const uint2 d = threefry2x32(seed ^ 0x9E3779B9u, step, gw, (uint32_t)i * (kHidden / 2) + (uint32_t)q);
+                    t.hidden[r * kHidden + 2 * q] = u01(d.x) - 0.5f;
+                    t.hidden[r * kHidden + 2 * q + 1] = u01(d.y) - 0.5f;
+                }
         }
     });
 }

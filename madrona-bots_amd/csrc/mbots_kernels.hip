@@ -16,6 +16,7 @@
 #include <hip/hip_ext.h>
 #include "mbots_kernels.hpp"
 #include <stdlib.h>
+#include <algorithm>
 #include "mbots_ray.hpp"
 
 namespace mbots {
@@ -1183,9 +1184,13 @@ __global__ __launch_bounds__(64 * kSensorWorlds, MB_SENSOR_BLOCKS) void sensor_k
 // f32 -- torch.cat's promotion of the five exported views: depth bytes as
 // uint8 (the semantic buffer when depth aliases it, B.1), health as the f32
 // reinterpretation of its int32 bits (B.2), semantic bytes as int8.  All N rows
-// (every species, species-major) in one pass; thread = one float of the output.
+// (every species, species-major) in one pass.  A block takes 64 rows: their
+// inputs are loaded coalesced into LDS (depth / semantic as 16-B granules),
+// then the block's 64 x 69 contiguous output floats are written coalesced, four
+// per thread as 16-B stores (HBM-bound: 84 B read + 276 B written per row).
 // ---------------------------------------------------------------------------
 constexpr int kObsDim = 69;
+constexpr int kObsRows = 64;
 __global__ __launch_bounds__(256) void construct_obs_kernel(const uint32_t *totals,
                                                             const uint8_t *depth,
                                                             const int8_t *sem,
@@ -1193,18 +1198,44 @@ __global__ __launch_bounds__(256) void construct_obs_kernel(const uint32_t *tota
                                                             const float *pos, const float *sur,
                                                             float *out, uint32_t out_rows)
 {
+    __shared__ uint4 s_dep[kObsRows * 2], s_sem[kObsRows * 2];
+    __shared__ int32_t s_hp[kObsRows];
+    __shared__ float2 s_pos[kObsRows], s_sur[kObsRows];
     const uint32_t N = min(totals[0], out_rows);
-    const size_t items = (size_t)N * kObsDim;
-    const size_t stride = (size_t)gridDim.x * blockDim.x;
-    for (size_t idx = (size_t)blockIdx.x * blockDim.x + threadIdx.x; idx < items; idx += stride) {
-        const uint32_t r = (uint32_t)(idx / kObsDim), c = (uint32_t)(idx - (size_t)r * kObsDim);
-        float v;
-        if (c < 32) v = (float)depth[(size_t)r * kSensor + c];
-        else if (c == 32) v = __int_as_float(health[r]);
-        else if (c < 35) v = pos[(size_t)r * 2 + (c - 33)];
-        else if (c < 67) v = (float)sem[(size_t)r * kSensor + (c - 35)];
-        else v = sur[(size_t)r * 2 + (c - 67)];
-        out[idx] = v;
+    const uint32_t nblk = (N + kObsRows - 1) / kObsRows;
+    const uint32_t t = threadIdx.x;
+    const uint8_t *sd = reinterpret_cast<const uint8_t *>(s_dep);
+    const int8_t *ss = reinterpret_cast<const int8_t *>(s_sem);
+    // output float (r, c) of the block's rows from the LDS image
+    auto val = [&](uint32_t i) {
+        const uint32_t r = i / kObsDim, c = i - r * kObsDim;
+        if (c < 32) return (float)sd[r * kSensor + c];
+        if (c == 32) return __int_as_float(s_hp[r]);
+        if (c < 35) return c == 33 ? s_pos[r].x : s_pos[r].y;
+        if (c < 67) return (float)ss[r * kSensor + (c - 35)];
+        return c == 67 ? s_sur[r].x : s_sur[r].y;
+    };
+    for (uint32_t b = blockIdx.x; b < nblk; b += gridDim.x) {
+        const uint32_t r0 = b * kObsRows, nr = min((uint32_t)kObsRows, N - r0);
+        if (t < 2 * nr) s_dep[t] = reinterpret_cast<const uint4 *>(depth + (size_t)r0 * kSensor)[t];
+        else if (t >= 128 && t - 128 < 2 * nr)
+            s_sem[t - 128] = reinterpret_cast<const uint4 *>(sem + (size_t)r0 * kSensor)[t - 128];
+        if (t < nr) {
+            s_hp[t] = health[r0 + t];
+            s_pos[t] = reinterpret_cast<const float2 *>(pos)[r0 + t];
+            s_sur[t] = reinterpret_cast<const float2 *>(sur)[r0 + t];
+        }
+        __syncthreads();
+        float *o = out + (size_t)r0 * kObsDim;
+        if (nr == (uint32_t)kObsRows && (reinterpret_cast<uintptr_t>(out) & 15u) == 0) {
+            // 64 x 69 floats = 1104 16-B granules
+            for (uint32_t g = t; g < kObsRows * kObsDim / 4; g += 256)
+                reinterpret_cast<float4 *>(o)[g] = make_float4(val(4 * g), val(4 * g + 1), val(4 * g + 2),
+                                                               val(4 * g + 3));
+        } else {
+            for (uint32_t i = t; i < nr * kObsDim; i += 256) o[i] = val(i);
+        }
+        __syncthreads();
     }
 }
 
@@ -1319,11 +1350,12 @@ __global__ __launch_bounds__(256) void synthetic_actions_kernel(SimState S, ObsT
         ap[0] = make_int2(k == 0, k == 1);
         ap[1] = make_int2(k == 2, k == 3);
         ap[2] = make_int2(k == 4, k == 5);
-        if (write_hidden) {
-            for (int j = 0; j < kHidden; ++j) {
-                const uint32_t hb = threefry2x32(seed ^ 0x9E3779B9u, step, gw,
-                                                 (uint32_t)i * kHidden + (uint32_t)j).x;
-                t.hidden[r * kHidden + j] = u01(hb) - 0.5f;
+        if (write_hidden) {   // both words of each draw: hidden[2k], hidden[2k + 1]
+            float4 *hp = reinterpret_cast<float4 *>(t.hidden + r * kHidden);
+            for (int q = 0; q < kHidden / 4; ++q) {
+                const uint2 a = threefry2x32(seed ^ 0x9E3779B9u, step, gw, (uint32_t)i * (kHidden / 2) + 2u * q);
+                const uint2 b = threefry2x32(seed ^ 0x9E3779B9u, step, gw, (uint32_t)i * (kHidden / 2) + 2u * q + 1u);
+                hp[q] = make_float4(u01(a.x) - 0.5f, u01(a.y) - 0.5f, u01(b.x) - 0.5f, u01(b.y) - 0.5f);
             }
         }
     }
@@ -1458,7 +1490,8 @@ hipError_t launch_construct_obs(const SimState &S, const ObsTable &t, int prev, 
     const bool fixd = (S.flags & kFlagFixDepth) != 0;
     const int8_t *sem = prev ? t.psem : t.sem;
     const uint8_t *depth = fixd ? (prev ? t.pdepth : t.depth) : reinterpret_cast<const uint8_t *>(sem);
-    hipLaunchKernelGGL(construct_obs_kernel, dim3(4096), dim3(256), 0, st, S.totals, depth, sem,
+    const unsigned blocks = (unsigned)std::min<uint64_t>((out_rows + kObsRows - 1) / kObsRows, 16384);
+    hipLaunchKernelGGL(construct_obs_kernel, dim3(std::max(blocks, 1u)), dim3(256), 0, st, S.totals, depth, sem,
                        prev && !lz ? t.phealth : t.health, prev && !lz ? t.ppos : t.pos,
                        prev && !lz ? t.psur : t.sur,
                        out, out_rows);

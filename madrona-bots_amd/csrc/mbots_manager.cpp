@@ -751,9 +751,10 @@ int mbots_construct_obs(mbots_handle *h, int32_t prev, float *out, uint64_t out_
     if (!prev && (rc = wait_sensor(h))) return rc;   // current semantic rows come from K3b
     if (prev && h->six_pending[h->tb] && (rc = materialize_prev(h, st))) return rc;
     if (prev && (rc = materialize_psem(h, st))) return rc;
-    HIP_TRY(mbots::launch_construct_obs(h->S, h->T[h->tb], prev, h->prev_lazy[h->tb] ? 1 : 0, out,
-                                        (uint32_t)out_rows, st));
-    return MBOTS_OK;
+    return timed(h, MBOTS_TK_OBS, st, [&] {
+        return mbots::launch_construct_obs(h->S, h->T[h->tb], prev, h->prev_lazy[h->tb] ? 1 : 0, out,
+                                           (uint32_t)out_rows, st);
+    });
 }
 
 int mbots_agent_steps(mbots_handle *h, uint64_t *out)

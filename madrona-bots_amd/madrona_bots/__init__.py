@@ -124,9 +124,10 @@ def _exec_mode(v):
         raise ValueError(f"unknown exec_mode {v}")
     return v
 
-# TK_* indices of mbots_kernel_times
+
 OBS_DIM = 69   # learn/env.py:19
-KERNELS = ("world_step", "scan", "export", "sensor", "shift", "actions", "move")
+# TK_* indices of mbots_kernel_times
+KERNELS = ("world_step", "scan", "export", "sensor", "shift", "actions", "move", "obs")
 
 
 class Tensor:
@@ -162,7 +163,6 @@ class Tensor:
         if t.data_ptr() != self._ptr:
             raise RuntimeError("madrona_bots: to_torch() produced a copy, expected a view")
         return t
-
 
     def _host_view(self):
         import numpy as np

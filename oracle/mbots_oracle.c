@@ -903,11 +903,13 @@ void orc_write_synthetic_actions(orc_sim *s, uint32_t seed, uint32_t step, int w
             uint32_t h = orc_action_hash(seed, step, gw, (uint32_t)i);
             uint32_t k = h % 6u;
             for (uint32_t j = 0; j < 6; ++j) c->action[r * 6 + j] = (j == k) ? 1 : 0;
-            if (write_hidden) {
-                for (uint32_t j = 0; j < ORC_HIDDEN; ++j) {
-                    uint32_t hb = orc_action_hash(seed ^ 0x9E3779B9u, step, gw,
-                                                  (uint32_t)i * ORC_HIDDEN + j);
-                    c->hidden[r * ORC_HIDDEN + j] = orc_sample_uniform(hb) - 0.5f;
+            if (write_hidden) {   /* both words of draw k: hidden[2k], hidden[2k + 1] */
+                for (uint32_t q = 0; q < ORC_HIDDEN / 2; ++q) {
+                    uint32_t kk[2] = {seed ^ 0x9E3779B9u, step};
+                    uint32_t cc[2] = {gw, (uint32_t)i * (ORC_HIDDEN / 2) + q}, hb[2];
+                    orc_threefry2x32(kk, cc, hb);
+                    c->hidden[r * ORC_HIDDEN + 2 * q] = orc_sample_uniform(hb[0]) - 0.5f;
+                    c->hidden[r * ORC_HIDDEN + 2 * q + 1] = orc_sample_uniform(hb[1]) - 0.5f;
                 }
             }
         }
