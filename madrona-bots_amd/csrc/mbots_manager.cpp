@@ -89,6 +89,8 @@ struct mbots_handle {
     bool six_lazy[2] = {false, false};
     bool prev_lazy[2] = {false, false};   // table half's six shift-owned Prev* columns are
                                           // still its current ones (lazy shift, K5)
+    int forced = 0;                   // deferred parts the caller's reads forced since the
+                                      // last step (kMove*): the next step prefetches them
     uint64_t steps = 0;               // steps run
     hipStream_t last_stream = nullptr;
     bool timing = false;
@@ -275,6 +277,14 @@ int materialize_psem(mbots_handle *h, hipStream_t st)
     if (rc) return rc;
     h->psem_pending[h->tb] = false;
     return MBOTS_OK;
+}
+
+// deferred parts still owed by the current half (kMove* bits)
+int pending_mask(const mbots_handle *h)
+{
+    const int tb = h->tb;
+    return (h->cur_ah_pending[tb] ? mbots::kMoveAH : 0) | (h->psem_pending[tb] ? mbots::kMoveSensor : 0) |
+           (h->ah_pending[tb] ? mbots::kMovePrevAH : 0) | (h->six_pending[tb] ? mbots::kMovePrev6 : 0);
 }
 
 int sync_totals(mbots_handle *h)
@@ -502,6 +512,16 @@ int mbots_step(mbots_handle *h, void *stream)
     int rc;
     const int par = h->parity;
     const int lazy = h->prev_lazy[h->tb] ? 1 : 0;
+    // the parts the caller's reads forced last step (a learner that reads the
+    // observation and PrevHiddenState between step and shift, as
+    // training_loop.py:47-88 does): moved right after this step's K3a, beside
+    // the sensor, instead of behind the wait for it (DESIGN.md "Prefetch")
+#ifdef MB_NO_FORK
+    const int prefetch = h->forced & ~mbots::kMoveSensor;
+#else
+    const int prefetch = h->forced;
+#endif
+    h->forced = 0;
     // no shift since the last step: its deferred Prev moves first
     if (h->six_pending[h->tb] && (rc = materialize_prev(h, st))) return rc;
     if ((rc = materialize_prev_ah(h, st))) return rc;
@@ -543,6 +563,10 @@ int mbots_step(mbots_handle *h, void *stream)
                     [&] { return mbots::launch_export_rows(h->S, nxt, 0, st); })))
         return rc;
 #endif
+    if (prefetch && (rc = timed(h, MBOTS_TK_MOVE, st, [&] {
+                         return mbots::launch_move(h->S, cur, nxt, lazy, prefetch, st);
+                     })))
+        return rc;
     ++h->steps;
     h->parity ^= 1;
     h->tb ^= 1;
@@ -555,6 +579,10 @@ int mbots_step(mbots_handle *h, void *stream)
     h->ah_pending[h->tb] = true;
     h->six_pending[h->tb] = true;
     h->six_lazy[h->tb] = lazy != 0;
+    if (prefetch & mbots::kMoveAH) h->cur_ah_pending[h->tb] = false;
+    if (prefetch & mbots::kMoveSensor) h->psem_pending[h->tb] = false;
+    if (prefetch & mbots::kMovePrevAH) h->ah_pending[h->tb] = false;
+    if (prefetch & mbots::kMovePrev6) h->six_pending[h->tb] = false;
     return MBOTS_OK;
 }
 
@@ -615,6 +643,7 @@ int mbots_export(mbots_handle *h, int32_t id, mbots_tensor *out)
     uint32_t N = 0;
     int rc = mbots_num_agents(h, &N);
     if (rc) return rc;
+    const int owed = pending_mask(h);
     switch (id) {
     case MBOTS_EXPORT_PREV_SPECIES: case MBOTS_EXPORT_PREV_POSITION: case MBOTS_EXPORT_PREV_HEALTH:
     case MBOTS_EXPORT_PREV_SURROUNDING: case MBOTS_EXPORT_PREV_REWARD: case MBOTS_EXPORT_PREV_STATS:
@@ -631,6 +660,7 @@ int mbots_export(mbots_handle *h, int32_t id, mbots_tensor *out)
         break;
     default: break;
     }
+    h->forced |= owed & ~pending_mask(h);
     const ObsTable &t = h->T[h->tb];
     const bool fixd = (h->cfg.flags & MBOTS_FLAG_FIX_DEPTH_ALIAS) != 0;
     void *p = nullptr;
@@ -695,7 +725,9 @@ int mbots_set_action(mbots_handle *h, uint32_t row, const int32_t action[6])
         memcpy(&h->cpu->table().action[(size_t)row * 6], action, 6 * sizeof(int32_t));
         return MBOTS_OK;
     }
+    const int owed = pending_mask(h);
     if ((rc = materialize_cur_ah(h, h->last_stream))) return rc;
+    h->forced |= owed & ~pending_mask(h);
     HIP_TRY(hipMemcpyAsync(h->T[h->tb].action + (size_t)row * 6, action, 6 * sizeof(int32_t),
                            hipMemcpyHostToDevice, h->last_stream));
     HIP_TRY(hipStreamSynchronize(h->last_stream));
@@ -729,8 +761,10 @@ int mbots_write_synthetic_actions(mbots_handle *h, uint32_t seed, uint32_t step,
     HIP_TRY(hipSetDevice(h->device));
     hipStream_t st = as_stream(stream);
     h->last_stream = st;
+    const int owed = pending_mask(h);
     int rc = materialize_cur_ah(h, st);
     if (rc) return rc;
+    h->forced |= owed & ~pending_mask(h);
     return timed(h, MBOTS_TK_ACTIONS, st, [&] {
         return mbots::launch_synthetic_actions(h->S, h->T[h->tb], seed, step, write_hidden, st);
     });
@@ -748,9 +782,11 @@ int mbots_construct_obs(mbots_handle *h, int32_t prev, float *out, uint64_t out_
     hipStream_t st = as_stream(stream);
     h->last_stream = st;
     int rc;
+    const int owed = pending_mask(h);
     if (!prev && (rc = wait_sensor(h))) return rc;   // current semantic rows come from K3b
     if (prev && h->six_pending[h->tb] && (rc = materialize_prev(h, st))) return rc;
     if (prev && (rc = materialize_psem(h, st))) return rc;
+    h->forced |= owed & ~pending_mask(h);
     return timed(h, MBOTS_TK_OBS, st, [&] {
         return mbots::launch_construct_obs(h->S, h->T[h->tb], prev, h->prev_lazy[h->tb] ? 1 : 0, out,
                                            (uint32_t)out_rows, st);
@@ -887,6 +923,7 @@ int mbots_load_checkpoint(mbots_handle *h, const void *src, uint64_t bytes)
     h->six_pending[0] = h->six_pending[1] = false;
     h->cur_ah_pending[0] = h->cur_ah_pending[1] = false;
     h->psem_pending[0] = h->psem_pending[1] = false;
+    h->forced = 0;
     h->steps = 1;
     hipStream_t st = nullptr;
     int rc = record_totals(h, st);
