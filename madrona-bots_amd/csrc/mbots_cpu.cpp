@@ -466,15 +466,15 @@ void Sim::sensor_world(uint32_t w, Table &nxt)
             const float u = ray_u(k), sgn = k < 24 ? 1.0f : -1.0f;
             const float dx = sgn * (h.x + u * h.y), dy = sgn * (h.y + u * (-h.x));
             const uint32_t kv = key[k];
-            const float oz = u2f(kv & ~0xFFu);
-            const uint32_t order = kv & 0xFFu;
+            const float oz = u2f(kv & ~kOrderMask);
+            const uint32_t order = kv & kOrderMask;
             const bool obj = (kv != kNoKey) && beats_wall(ax, ay, dx, dy, oz);
             nxt.sem[r * kSensor + k] =
                 (int8_t)(obj ? (order < kOrderAgent ? 6 : species_[base + order - kOrderAgent]) : 5);
             if (fixd) nxt.depth[r * kSensor + k] = depth_u8(obj ? oz : wall_z(ax, ay, dx, dy));
         }
-        const uint32_t kv = key[kSensor], order = kv & 0xFFu;
-        const bool agent = kv != kNoKey && order >= kOrderAgent && beats_wall(ax, ay, h.x, h.y, u2f(kv & ~0xFFu));
+        const uint32_t kv = key[kSensor], order = kv & kOrderMask;
+        const bool agent = kv != kNoKey && order >= kOrderAgent && beats_wall(ax, ay, h.x, h.y, u2f(kv & ~kOrderMask));
         finder_[base + i] = agent ? (int32_t)(order - kOrderAgent) : -1;
     }
 }

@@ -112,20 +112,23 @@ __device__ __forceinline__ uint64_t food_pack(const uint16_t *pk)
 // ---------------------------------------------------------------------------
 // Per-world LDS image used by the world-step kernel
 // ---------------------------------------------------------------------------
+// kCap: the slot capacity class (128: the default, 8 blocks per CU; 256)
+template <int kCap>
 struct WorldLDS {
-    float x[kMaxCap], y[kMaxCap], rw[kMaxCap], rz[kMaxCap];
-    int32_t accum[kMaxCap];
-    int8_t species[kMaxCap], finder[kMaxCap];
-    uint8_t flags[kMaxCap];
+    float x[kCap], y[kCap], rw[kCap], rz[kCap];
+    int32_t accum[kCap];
+    int16_t finder[kCap];
+    int8_t species[kCap];
+    uint8_t flags[kCap];
     // healthSync's cell keys / package takes (slots < n0) share storage with the
     // surroundings written after it (children/respawns, slots >= n0, only
     // touch the sur half)
     union {
-        struct { int32_t key[kMaxCap]; int32_t take[kMaxCap]; };
-        struct { float sur0[kMaxCap]; float sur1[kMaxCap]; };
+        struct { int32_t key[kCap]; int32_t take[kCap]; };
+        struct { float sur0[kCap]; float sur1[kCap]; };
     };
     uint16_t food[kNumPkg];
-    uint32_t chunk[kNumChunks];   // ChunkInfo: numAgents << 16 | totalSpeed (<= 128 x 2)
+    uint32_t chunk[kNumChunks];   // ChunkInfo: numAgents << 16 | totalSpeed (<= 256 x 2)
     uint32_t cnt[kNumSpecies], hsum[kNumSpecies];
     int32_t need[kNumSpecies];
     int32_t scount[kNumSpecies];
@@ -147,7 +150,8 @@ __device__ __forceinline__ uint32_t rng_draw(uint2 key, uint32_t ctr)
     return threefry2x32(key.x, key.y, ctr, 0u).x;
 }
 
-__device__ __forceinline__ void init_slot(WorldLDS &L, int s, float x, float y, int32_t sp,
+template <int kCap>
+__device__ __forceinline__ void init_slot(WorldLDS<kCap> &L, int s, float x, float y, int32_t sp,
                                           int32_t h)
 {
     L.x[s] = x;
@@ -168,12 +172,15 @@ __device__ __forceinline__ void init_slot(WorldLDS &L, int s, float x, float y, 
 // speciesInfoSync + respawn, and the per-world compaction of
 // SortArchetypeNode<Agent, WorldID> (sim.cpp:1061-1132).
 // ---------------------------------------------------------------------------
-__device__ void world_step(SimState &S, const ObsTable &cur, WorldLDS &L, uint32_t w,
+template <int kCap>
+__device__ void world_step(SimState &S, const ObsTable &cur, WorldLDS<kCap> &L, uint32_t w,
                            uint32_t lane);
 
-__global__ __launch_bounds__(256, 8) void world_step_kernel(SimState S, ObsTable cur, int parity)
+template <int kCap>
+__global__ __launch_bounds__(256, kCap <= 128 ? 8 : 4) void world_step_kernel(SimState S, ObsTable cur,
+                                                                              int parity)
 {
-    __shared__ WorldLDS lds[kWorldsPerBlock];
+    __shared__ WorldLDS<kCap> lds[kWorldsPerBlock];
     __shared__ int32_t blk[kWorldsPerBlock][5];
     const uint32_t wv = threadIdx.x >> 6;
     const uint32_t lane = threadIdx.x & 63u;
@@ -193,19 +200,23 @@ __global__ __launch_bounds__(256, 8) void world_step_kernel(SimState S, ObsTable
     }
 }
 
-__device__ void world_step(SimState &S, const ObsTable &cur, WorldLDS &L, uint32_t w,
+template <int kCap>
+__device__ void world_step(SimState &S, const ObsTable &cur, WorldLDS<kCap> &L, uint32_t w,
                            uint32_t lane)
 {
+    constexpr int kG = kCap / 64;   // 64-slot groups
     const uint32_t cap = S.cap;
     const size_t base = (size_t)w * cap;
     const int n0 = uniform(S.n[w]);
 
     // ---- stage the world in LDS; slot `lane`'s action row is fetched now and
     // consumed after addFood (its latency hides behind that serial phase) ----
-    // The old export rows stay in registers (slot lane: row_lo, 64 + lane:
-    // row_hi): only the slot's own lane reads them (action fetch, compaction).
+    // The old export rows stay in registers (rows[g]: slot 64 g + lane): only
+    // the slot's own lane reads them (action fetch, compaction).
     int2 pa0 = make_int2(0, 0), pa1 = pa0, pa2 = pa0;
-    int32_t row_lo = -1, row_hi = -1;
+    int32_t rows[kG];
+#pragma unroll
+    for (int g = 0; g < kG; ++g) rows[g] = -1;
     // per-world records: issued with the first batch (none depends on n0)
     const uint64_t food_rec = lane < kNumChunks ? S.food[(size_t)w * kNumChunks + lane] : 0ull;
     const uint2 key = S.key[w];
@@ -222,7 +233,7 @@ __device__ void world_step(SimState &S, const ObsTable &cur, WorldLDS &L, uint32
         const int32_t sp = in ? S.species[i] : 0, hp = in ? S.health[i] : 0;
         const int32_t fd = in ? S.finder[i] : -1;
         if ((int)lane < n0) {
-            row_lo = row;
+            rows[0] = row;
             if (row >= 0) {
                 const int2 *ap = reinterpret_cast<const int2 *>(cur.action + (size_t)row * 6);
                 pa0 = ap[0]; pa1 = ap[1]; pa2 = ap[2];
@@ -233,26 +244,25 @@ __device__ void world_step(SimState &S, const ObsTable &cur, WorldLDS &L, uint32
             L.rz[lane] = rz;
             L.species[lane] = (int8_t)sp;
             L.accum[lane] = hp;
-            L.finder[lane] = (int8_t)fd;
+            L.finder[lane] = (int16_t)fd;
             L.flags[lane] = (uint8_t)F_ALIVE;
         }
     }
-    for (int i = 64 + lane; i < n0; i += 64) {
-        const int32_t row = S.obsrow[base + i];
-        if (i < 64) row_lo = row;
-        else row_hi = row;
-        if (i < 64 && row >= 0) {
-            const int2 *ap = reinterpret_cast<const int2 *>(cur.action + (size_t)row * 6);
-            pa0 = ap[0]; pa1 = ap[1]; pa2 = ap[2];
+#pragma unroll
+    for (int g = 1; g < kG; ++g) {   // slots past 64
+        const int i = 64 * g + (int)lane;
+        if (64 * g >= n0) break;
+        if (i < n0) {
+            rows[g] = S.obsrow[base + i];
+            L.x[i] = S.x[base + i];
+            L.y[i] = S.y[base + i];
+            L.rw[i] = S.rw[base + i];
+            L.rz[i] = S.rz[base + i];
+            L.species[i] = (int8_t)S.species[base + i];
+            L.accum[i] = S.health[base + i];
+            L.finder[i] = (int16_t)S.finder[base + i];
+            L.flags[i] = (uint8_t)F_ALIVE;
         }
-        L.x[i] = S.x[base + i];
-        L.y[i] = S.y[base + i];
-        L.rw[i] = S.rw[base + i];
-        L.rz[i] = S.rz[base + i];
-        L.species[i] = (int8_t)S.species[base + i];
-        L.accum[i] = S.health[base + i];
-        L.finder[i] = (int8_t)S.finder[base + i];
-        L.flags[i] = (uint8_t)F_ALIVE;
     }
     if (lane < kNumChunks) food_unpack(food_rec, &L.food[lane * kMaxPkg]);
     if (lane < kNumChunks) L.chunk[lane] = 0u;   // resetChunkInfoSystem
@@ -300,10 +310,14 @@ __device__ void world_step(SimState &S, const ObsTable &cur, WorldLDS &L, uint32
     }
 
     // ---- actionSystem (sim.cpp:419-502) ----
-    for (int i = lane; i < n0; i += 64) {
+#pragma unroll
+    for (int g = 0; g < kG; ++g) {
+        const int i = 64 * g + (int)lane;
+        if (64 * g >= n0) break;
+        if (i >= n0) continue;
         int2 a0 = pa0, a1 = pa1, a2 = pa2;
-        const int32_t row = i < 64 ? row_lo : row_hi;
-        if (i >= 64 && row >= 0) {
+        const int32_t row = rows[g];
+        if (g > 0 && row >= 0) {
             const int2 *ap = reinterpret_cast<const int2 *>(cur.action + (size_t)row * 6);
             a0 = ap[0]; a1 = ap[1]; a2 = ap[2];
         }
@@ -473,7 +487,10 @@ __device__ void world_step(SimState &S, const ObsTable &cur, WorldLDS &L, uint32
 
     // ---- compaction (SortArchetypeNode<Agent, WorldID>, sim.cpp:1129) ----
     int nn = 0;
-    for (int b = 0; b < n2; b += 64) {
+#pragma unroll
+    for (int g = 0; g < kG; ++g) {
+        const int b = 64 * g;
+        if (b >= n2) break;
         const int i = b + (int)lane;
         const bool alive = i < n2 && (L.flags[i] & F_ALIVE);
         const uint64_t m = ballot64(alive);
@@ -485,7 +502,7 @@ __device__ void world_step(SimState &S, const ObsTable &cur, WorldLDS &L, uint32
             S.rz_out[d] = L.rz[i];
             S.species_out[d] = L.species[i];
             S.health[d] = L.accum[i];
-            S.obsrow_out[d] = i < n0 ? (b == 0 ? row_lo : row_hi) : -1;   // newborns: no row
+            S.obsrow_out[d] = i < n0 ? rows[g] : -1;   // newborns: no row
             S.sur0[d] = L.sur0[i];
             S.sur1[d] = L.sur1[i];
             S.stats[d] = L.flags[i] & F_STATS;
@@ -770,7 +787,7 @@ __global__ __launch_bounds__(256) void shift_move_kernel(const uint32_t *totals,
 // r = (hy, -hx)) ray h + u r meets a circle iff
 //     q(u) = (A u - 2 l f) u + C <= 0,   A = f^2 - 1,  C = l^2 - 1,
 // ahead of the origin iff f + u l > 0 (backward camera: < 0); view depth
-// z = f - 1 (>= 0, 15-bit mantissa).  Per ray the lexicographic minimum of
+// z = f - 1 (>= 0, 14-bit mantissa).  Per ray the lexicographic minimum of
 // (z, order) over objects (food 1 + k, agents 64 + slot) is seen iff it beats
 // the wall (z * d < X - o per axis), else the wall (order 0).
 //
@@ -780,7 +797,7 @@ __global__ __launch_bounds__(256) void shift_move_kernel(const uint32_t *totals,
 //      their (f, l) are ballot-compacted into a queue;
 //  P2  per survivor: approximate roots of q bound its candidate pixels; <= 2
 //      pixels + the finder run the exact predicate inline and ds_min_u32 the
-//      32-bit key (z with its low 8 mantissa bits replaced by the object
+//      32-bit key (z with its low 9 mantissa bits replaced by the object
 //      order); nearer / wider pairs go to a wide list;
 //  W   wide pairs: two per wave, one lane per ray;
 //  out per (agent, ray): key vs wall -> semantic / depth bytes; finder slot.
@@ -805,11 +822,12 @@ constexpr float kFoodFar = 2.5f;
 constexpr int kFoodInline = 6;
 constexpr float kFarCull = 5.0f;               // P1 angular cull from this |f| on
 
+template <int kCap>
 struct SensorLDS {
-    float2 obj[kMaxFood + kMaxCap];           // positions: food, then agents
+    float2 obj[kMaxFood + kCap];              // positions: food, then agents
     float2 frot[kMaxFood];                    // food squares' (cos, sin)
-    float2 hd[kMaxCap];                       // agent headings
-    int8_t sp[kMaxCap];
+    float2 hd[kCap];                          // agent headings
+    int8_t sp[kCap];
     alignas(16) uint32_t key[kKeyAgents * kKeyStride];
     uint32_t qcode[kQueueCap + 1];            // P1 survivors: agent | object << 11 (+ a
                                               // sink slot for the branch-free write); a
@@ -830,7 +848,8 @@ __constant__ float kURay[kSensor] = {MB_U4(0),  MB_U4(4),  MB_U4(8),  MB_U4(12),
 #undef MB_U4
 
 // (f, l) of object j in agent i's frame; order of the object
-__device__ __forceinline__ void pair_fl(const SensorLDS &L, int nf, int i, int j, float &f,
+template <class LDS>
+__device__ __forceinline__ void pair_fl(const LDS &L, int nf, int i, int j, float &f,
                                         float &l, uint32_t &order)
 {
     const float2 a = L.obj[nf + i];
@@ -844,7 +863,8 @@ __device__ __forceinline__ void pair_fl(const SensorLDS &L, int nf, int i, int j
 
 // W: wide pairs qcode[q0, q0 + cnt), two per wave (32 lanes each: rays 0..31,
 // lane 0 of each half also takes the finder ray)
-__device__ __forceinline__ void run_wide(SensorLDS &L, int nf, int a0, int q0, int cnt)
+template <class LDS>
+__device__ __forceinline__ void run_wide(LDS &L, int nf, int a0, int q0, int cnt)
 {
     const int lane = (int)__lane_id();
     for (int e0 = 0; e0 < cnt; e0 += 2) {
@@ -874,7 +894,8 @@ __device__ __forceinline__ void run_wide(SensorLDS &L, int nf, int a0, int q0, i
 
 // P2: survivors [q0, q0 + cnt): approximate roots bound the candidate pixels;
 // <= 2 pixels + the finder are tested inline, wider pairs go to the wide list
-__device__ __forceinline__ void run_survivors(SensorLDS &L, int nf, int a0, int q0, int cnt)
+template <class LDS>
+__device__ __forceinline__ void run_survivors(LDS &L, int nf, int a0, int q0, int cnt)
 {
     const int lane = (int)__lane_id();
     bool wide = false;
@@ -999,10 +1020,12 @@ constexpr int kSensorWorlds = MB_SENSOR_WPB;   // worlds (waves) per sensor bloc
 // (<= 4096), where one wave per world leaves SIMDs idle and the step waits on
 // the latency of one world's serial chunk loop (4 waves per world: step -8 % at
 // 4096 worlds; 2 waves: -5 %; no gain at 8192).
-template <bool kDepth, int kSplit>
-__global__ __launch_bounds__(64 * kSensorWorlds, MB_SENSOR_BLOCKS) void sensor_kernel(SimState S, ObsTable nxt)
+template <bool kDepth, int kSplit, int kCap>
+__global__ __launch_bounds__(64 * kSensorWorlds, kCap <= 128 ? MB_SENSOR_BLOCKS : 4) void sensor_kernel(SimState S,
+                                                                                                  ObsTable nxt)
 {
-    __shared__ SensorLDS lds[kSensorWorlds];
+    constexpr int kG = kCap / 64;   // 64-slot groups
+    __shared__ SensorLDS<kCap> lds[kSensorWorlds];
     const uint32_t wv = threadIdx.x >> 6;
     const uint32_t lane = threadIdx.x & 63u;
     static_assert(kSensorWorlds % kSplit == 0, "split must divide the block's waves");
@@ -1010,7 +1033,7 @@ __global__ __launch_bounds__(64 * kSensorWorlds, MB_SENSOR_BLOCKS) void sensor_k
     constexpr int kChunkStep = kKeyAgents * kSplit;
     const int kChunk0 = (int)(wv % kSplit) * kKeyAgents;
     if (w >= S.W) return;
-    SensorLDS &L = lds[wv];
+    SensorLDS<kCap> &L = lds[wv];
     constexpr bool depth = kDepth;
     if (lane < kSensor) L.u[lane] = kURay[lane];
     SensorPrefetch pf;
@@ -1032,23 +1055,19 @@ __global__ __launch_bounds__(64 * kSensorWorlds, MB_SENSOR_BLOCKS) void sensor_k
     }
     // export rows (K3a's rule, computed here so the sensor need not wait for
     // K3a): row_base[w][species] + rank among the world's slots of that
-    // species.  They stay in registers: lane s holds slot s (row_lo) and 64 + s
-    // (row_hi).
+    // species.  They stay in registers: rows[g] of lane s is slot 64 g + s.
     const int4 rb = cur.rb;
-    int row_lo, row_hi = 0;
-    int c1, c2, c3, c4;
-    {
-        const int sp = (int)lane < n ? cur.sp : 0;
-        const uint64_t m1 = ballot64(sp == 1), m2 = ballot64(sp == 2);
-        const uint64_t m3 = ballot64(sp == 3), m4 = ballot64(sp == 4);
-        row_lo = sp == 1 ? rb.x + (int)rank_below(m1) : sp == 2 ? rb.y + (int)rank_below(m2)
-               : sp == 3 ? rb.z + (int)rank_below(m3) : rb.w + (int)rank_below(m4);
-        c1 = __popcll(m1); c2 = __popcll(m2); c3 = __popcll(m3); c4 = __popcll(m4);
-    }
-    if (n > 64) {   // slots past 64: loaded here
-        const int i = 64 + (int)lane;
+    int rows[kG];
+    int c1 = 0, c2 = 0, c3 = 0, c4 = 0;
+#pragma unroll
+    for (int g = 0; g < kG; ++g) {
+        rows[g] = 0;
+        if (g > 0 && 64 * g >= n) continue;
+        const int i = 64 * g + (int)lane;
         int sp = 0;
-        if (i < n) {
+        if (g == 0) {
+            sp = (int)lane < n ? cur.sp : 0;
+        } else if (i < n) {   // slots past 64: loaded here
             float hx, hy;
             heading(S.rw[base + i], S.rz[base + i], hx, hy);
             L.obj[nf + i] = make_float2(S.x[base + i], S.y[base + i]);
@@ -1058,8 +1077,9 @@ __global__ __launch_bounds__(64 * kSensorWorlds, MB_SENSOR_BLOCKS) void sensor_k
         }
         const uint64_t m1 = ballot64(sp == 1), m2 = ballot64(sp == 2);
         const uint64_t m3 = ballot64(sp == 3), m4 = ballot64(sp == 4);
-        row_hi = sp == 1 ? rb.x + c1 + (int)rank_below(m1) : sp == 2 ? rb.y + c2 + (int)rank_below(m2)
-               : sp == 3 ? rb.z + c3 + (int)rank_below(m3) : rb.w + c4 + (int)rank_below(m4);
+        rows[g] = sp == 1 ? rb.x + c1 + (int)rank_below(m1) : sp == 2 ? rb.y + c2 + (int)rank_below(m2)
+                : sp == 3 ? rb.z + c3 + (int)rank_below(m3) : rb.w + c4 + (int)rank_below(m4);
+        c1 += __popcll(m1); c2 += __popcll(m2); c3 += __popcll(m3); c4 += __popcll(m4);
     }
     const int nobj = nf + n;
     wave_sync();
@@ -1135,7 +1155,16 @@ __global__ __launch_bounds__(64 * kSensorWorlds, MB_SENSOR_BLOCKS) void sensor_k
             const float2 p = L.obj[nf + i], h = L.hd[i];
             const uint4 kv4 = *reinterpret_cast<const uint4 *>(&L.key[cc * kKeyStride + 4 * g]);
             const float4 u4 = *reinterpret_cast<const float4 *>(&L.u[4 * g]);
-            const int r = a0 < 64 ? __shfl(row_lo, i & 63) : __shfl(row_hi, i & 63);
+            // the chunk's 64-slot group (8 | 64: one group per chunk), a uniform branch
+            int r;
+            if constexpr (kG == 2) {
+                r = a0 < 64 ? __shfl(rows[0], i & 63) : __shfl(rows[1], i & 63);
+            } else {
+                r = __shfl(rows[0], i & 63);
+#pragma unroll
+                for (int g = 1; g < kG; ++g)
+                    if ((a0 >> 6) == g) r = __shfl(rows[g], i & 63);
+            }
             const float sgn = g < 6 ? 1.0f : -1.0f;
             const uint32_t kvs[4] = {kv4.x, kv4.y, kv4.z, kv4.w};
             const float us[4] = {u4.x, u4.y, u4.z, u4.w};
@@ -1145,10 +1174,10 @@ __global__ __launch_bounds__(64 * kSensorWorlds, MB_SENSOR_BLOCKS) void sensor_k
                 const float u = us[t];
                 const float dx = sgn * (h.x + u * h.y), dy = sgn * (h.y + u * (-h.x));
                 const uint32_t kv = kvs[t];
-                const float oz = __uint_as_float(kv & ~0xFFu);
-                const uint32_t order = kv & 0xFFu;
+                const float oz = __uint_as_float(kv & ~kOrderMask);
+                const uint32_t order = kv & kOrderMask;
                 const bool obj = (kv != kNoKey) & beats_wall(p.x, p.y, dx, dy, oz);
-                const int spv = (int)L.sp[min((int)(order - kOrderAgent), n - 1) & 127];
+                const int spv = (int)L.sp[min((int)(order - kOrderAgent), n - 1) & (kCap - 1)];
                 const int sem = obj ? (order < kOrderAgent ? 6 : spv) : 5;
                 semv |= (uint32_t)(uint8_t)(int8_t)sem << (8 * t);
                 if (depth) {
@@ -1166,9 +1195,9 @@ __global__ __launch_bounds__(64 * kSensorWorlds, MB_SENSOR_BLOCKS) void sensor_k
             const int i = a0 + (int)lane;
             const float2 p = L.obj[nf + i], h = L.hd[i];
             const uint32_t kv = L.key[lane * kKeyStride + kSensor];
-            const uint32_t order = kv & 0xFFu;
+            const uint32_t order = kv & kOrderMask;
             const bool agent = (kv != kNoKey) & (order >= kOrderAgent) &&
-                               beats_wall(p.x, p.y, h.x, h.y, __uint_as_float(kv & ~0xFFu));
+                               beats_wall(p.x, p.y, h.x, h.y, __uint_as_float(kv & ~kOrderMask));
             S.finder[base + i] = agent ? (int32_t)(order - kOrderAgent) : -1;
         }
         wave_sync();
@@ -1392,7 +1421,10 @@ hipError_t launch_tile_sum(const SimState &S, int parity, hipStream_t st)
 }
 hipError_t launch_world_step(const SimState &S, const ObsTable &cur, int parity, hipStream_t st)
 {
-    hipLaunchKernelGGL(world_step_kernel, dim3(world_blocks(S.W)), dim3(256), 0, st, S, cur, parity);
+    if (S.cap <= 128)
+        hipLaunchKernelGGL(world_step_kernel<128>, dim3(world_blocks(S.W)), dim3(256), 0, st, S, cur, parity);
+    else
+        hipLaunchKernelGGL(world_step_kernel<256>, dim3(world_blocks(S.W)), dim3(256), 0, st, S, cur, parity);
     return hipGetLastError();
 }
 hipError_t launch_scan(const SimState &S, int parity, hipStream_t st, hipEvent_t done)
@@ -1454,20 +1486,26 @@ hipError_t launch_move(const SimState &S, const ObsTable &cur, const ObsTable &n
         hipLaunchKernelGGL(move_kernel, dim3(bx, k), dim3(256), 0, st, S.totals, S.src_of, m);
     return hipGetLastError();
 }
-hipError_t launch_sensor(const SimState &S, const ObsTable &nxt, hipStream_t st, hipEvent_t done)
+template <int kCap>
+static void launch_sensor_cap(const SimState &S, const ObsTable &nxt, hipStream_t st, hipEvent_t done)
 {
     const bool fixd = (S.flags & kFlagFixDepth) != 0;
     const dim3 blk(64 * kSensorWorlds);
     if (S.W <= (uint32_t)MB_SENSOR_SPLIT_MAX) {   // small: MB_SENSOR_SPLIT waves per world
         constexpr int kWpb = kSensorWorlds / MB_SENSOR_SPLIT;
         const dim3 grid((S.W + kWpb - 1) / kWpb);
-        if (fixd) hipExtLaunchKernelGGL((sensor_kernel<true, MB_SENSOR_SPLIT>), grid, blk, 0u, st, nullptr, done, 0u, S, nxt);
-        else hipExtLaunchKernelGGL((sensor_kernel<false, MB_SENSOR_SPLIT>), grid, blk, 0u, st, nullptr, done, 0u, S, nxt);
+        if (fixd) hipExtLaunchKernelGGL((sensor_kernel<true, MB_SENSOR_SPLIT, kCap>), grid, blk, 0u, st, nullptr, done, 0u, S, nxt);
+        else hipExtLaunchKernelGGL((sensor_kernel<false, MB_SENSOR_SPLIT, kCap>), grid, blk, 0u, st, nullptr, done, 0u, S, nxt);
     } else {
         const dim3 grid((S.W + kSensorWorlds - 1) / kSensorWorlds);
-        if (fixd) hipExtLaunchKernelGGL((sensor_kernel<true, 1>), grid, blk, 0u, st, nullptr, done, 0u, S, nxt);
-        else hipExtLaunchKernelGGL((sensor_kernel<false, 1>), grid, blk, 0u, st, nullptr, done, 0u, S, nxt);
+        if (fixd) hipExtLaunchKernelGGL((sensor_kernel<true, 1, kCap>), grid, blk, 0u, st, nullptr, done, 0u, S, nxt);
+        else hipExtLaunchKernelGGL((sensor_kernel<false, 1, kCap>), grid, blk, 0u, st, nullptr, done, 0u, S, nxt);
     }
+}
+hipError_t launch_sensor(const SimState &S, const ObsTable &nxt, hipStream_t st, hipEvent_t done)
+{
+    if (S.cap <= 128) launch_sensor_cap<128>(S, nxt, st, done);
+    else launch_sensor_cap<256>(S, nxt, st, done);
     return hipGetLastError();
 }
 hipError_t launch_shift(const SimState &S, const ObsTable &t, int mode, hipStream_t st)

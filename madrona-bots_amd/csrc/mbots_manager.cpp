@@ -365,7 +365,7 @@ int mbots_create(const mbots_config *cfg_in, mbots_handle **out)
     if (cfg.sensor_size != (uint32_t)mbots::kSensor)
         return fail(MBOTS_E_INVALID, "sensor_size must be 32 (mgr.hpp:19, entry.cpp:27)");
     if (cfg.agent_capacity > (uint32_t)mbots::kMaxCap || cfg.agent_capacity < 4)
-        return fail(MBOTS_E_INVALID, "agent_capacity must be in [4, 128]");
+        return fail(MBOTS_E_INVALID, "agent_capacity must be in [4, 256]");
     if (cfg.init_num_agents_per_world > cfg.agent_capacity)
         return fail(MBOTS_E_INVALID, "init_num_agents_per_world exceeds agent_capacity");
     if (cfg.init_num_agents_per_world < (uint32_t)mbots::kNumSpecies)

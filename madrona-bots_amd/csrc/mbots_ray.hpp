@@ -11,16 +11,19 @@ constexpr int kMaxFood = kFoodCap + 2;        // live packages == currentNumFood
 constexpr uint32_t kOrderFood = 1u;           // object order: wall 0, food 1.., agents 64..
 constexpr uint32_t kOrderAgent = 64u;
 constexpr uint32_t kNoKey = 0xFFFFFFFFu;
+// a key is the depth's float bits with the low 9 mantissa bits replaced by the
+// object order (food 1 + k, agents 64 + slot < 320): 14 mantissa bits of depth
+constexpr uint32_t kOrderMask = 0x1FFu;
 
 constexpr float kInLo = 0.0f + 0.2f;          // inner arena rectangle (walls, sim.cpp:157-194)
 constexpr float kInHiX = 128.0f - 0.2f;
 constexpr float kInHiY = 96.0f - 0.2f;
 
 MB_HD float max0(float x) { return x > 0.0f ? x : 0.0f; }
-MB_HD float zq(float z) { return u2f(f2u(z) & ~0xFFu); }
+MB_HD float zq(float z) { return u2f(f2u(z) & ~kOrderMask); }
 MB_HD uint32_t zkey(float z, uint32_t order)
 {
-    return (f2u(z) & ~0xFFu) | order;
+    return (f2u(z) & ~kOrderMask) | order;
 }
 
 // predicates below use non-short-circuit & | so they compile to VALU selects,

@@ -523,7 +523,7 @@ static void world_phase_c(orc_sim *s, uint32_t wi)
 /* lies ahead of the ray iff f + u l > 0 (backward camera: < 0).  Live food   */
 /* packages are rotated +-1 squares (raster_box below).  Depth is view-space  */
 /* z: z = f - 1 for circles, the nearest corner's for squares (clamped at 0,  */
-/* 15-bit mantissa: zq), the ray's                                           */
+/* 14-bit mantissa: zq), the ray's                                           */
 /* exit from the inner arena rectangle for the walls.  Each pixel takes the   */
 /* lexicographic minimum of (z, order): walls 0, food 1 + k, agents 64 + slot.*/
 /* ------------------------------------------------------------------------ */
@@ -572,13 +572,14 @@ static float wall_z(float ox, float oy, float dx, float dy)
 
 static inline float max0(float x) { return x > 0.0f ? x : 0.0f; }
 
-/* object depths keep 15 mantissa bits (the low 8 carry the object order in
- * the HIP kernel's 32-bit z-buffer key); floor(z) is unchanged for z < 2^15 */
+/* object depths keep 14 mantissa bits (the low 9 carry the object order in
+ * the HIP kernel's 32-bit z-buffer key: food 1 + k, agents 64 + slot < 320);
+ * floor(z) is unchanged for z < 2^14 */
 static inline float zq(float z)
 {
     uint32_t b;
     memcpy(&b, &z, 4);
-    b &= ~0xFFu;
+    b &= ~0x1FFu;
     memcpy(&z, &b, 4);
     return z;
 }

@@ -151,3 +151,29 @@ def _same(h, c, where):
             a = getattr(h, name)(prev).to_torch().cpu()
             b = getattr(c, name)(prev).to_torch()
             assert torch.equal(a.view(torch.uint8), b.view(torch.uint8)), (where, name, prev)
+
+
+def test_breed_heavy_to_capacity_256():
+    """A breed-heavy stream fills worlds to 256 slots; births past it are
+    dropped and counted exactly as the oracle does."""
+    W = 16
+    mgr = _mgr(W, agent_capacity=256)
+    orc = pyoracle.OracleSim(W, 69, 32, cap=256, num_threads=4)
+    for t in range(40):
+        g = torch.Generator().manual_seed(1000 + t)
+        n = mgr.num_agents()
+        r = torch.randint(0, 8, (n,), generator=g)
+        a = torch.zeros((n, 6), dtype=torch.int32)
+        a[r < 4, 5] = 1
+        a[(r >= 4) & (r < 6), 0] = 1
+        a[r == 6, 2] = 1
+        a[r == 7, 3] = 1
+        mgr.action_tensor(False).to_torch().copy_(a)
+        orc.column(pyoracle.COL_ACTION)[:] = a.numpy()
+        mgr.step()
+        orc.step()
+        errs = compare(mgr, orc, f"step {t}")
+        assert not errs, errs[:5]
+        mgr.shift_observations()
+        orc.shift_observations()
+    assert mgr.overflow() == orc.overflow() > 0
