@@ -156,7 +156,8 @@ def reference_loop(W, args, rank, world_size, dev, distributed, label):
     """learn/training_loop.py:36-137 without the learner math (out of scope),
     one rank's shard of W worlds; returns the line's dict."""
     import madrona_bots as mb
-    m = mb.SimManager(dev.index, W, SEED, AGENTS_PER_WORLD, world_offset=rank * W)
+    m = mb.SimManager(dev.index, W, SEED, AGENTS_PER_WORLD, world_offset=rank * W,
+                      shard_ghost=rank < world_size - 1)
 
     def one(t):
         m.step()                                             # :36
@@ -261,7 +262,10 @@ def main():
 
     import madrona_bots as mb
     W = args.worlds
-    mgr = mb.SimManager(dev_index, W, SEED, AGENTS_PER_WORLD, world_offset=rank * W)
+    # every rank but the last steps a ghost of the next rank's first world, so the
+    # faithful B.3 reward of its last world equals one device's (sim.cpp:943)
+    ghost = rank < world_size - 1
+    mgr = mb.SimManager(dev_index, W, SEED, AGENTS_PER_WORLD, world_offset=rank * W, shard_ghost=ghost)
 
     gather_s = [0.0]
 
@@ -369,7 +373,9 @@ def main():
                        "worlds_per_gpu": W, "total_worlds": W * world_size,
                        "mean_agents_per_world": mean_agents / W,
                        "world_steps_per_s": W * world_size * args.steps / elapsed,
-                       "parallelism": f"world-shard x{world_size}, no collective"},
+                       "parallelism": f"world-shard x{world_size}, no collective"
+                                      + (" (+1 ghost world on ranks 0..N-2: faithful B.3)"
+                                         if world_size > 1 else "")},
         }
         nb = algorithmic_bytes(mean_agents, W)
         achieved = nb / (span_ms * 1e-3) / 1e9

@@ -34,6 +34,14 @@ extern "C" {
 /* Manager::Config flags (build extensions; default 0 = reference-faithful) */
 #define MBOTS_FLAG_REWARD_FIXED     0x1u  /* rewards[speciesID-1] (fixes sim.cpp:943) */
 #define MBOTS_FLAG_FIX_DEPTH_ALIAS  0x2u  /* depth_tensor exports real depth (sim.cpp:102-112) */
+/* shard ghost: also step world world_offset + num_worlds (the next shard's
+ * first world), never exported, so the faithful rewards[speciesID] of the
+ * shard's last world reads the same SpeciesInfo row as on one device
+ * (sim.cpp:943).  The ghost's agents act on what
+ * mbots_write_synthetic_actions writes (the identity-keyed stream is keyed by
+ * global world, so with it N shards == one device exactly).  Every shard but
+ * the last sets it. */
+#define MBOTS_FLAG_SHARD_GHOST      0x4u
 
 /* execution modes (madrona::ExecMode; the reference's callers pick CPU when
  * no GPU is present, learn/env.py:12-15) */

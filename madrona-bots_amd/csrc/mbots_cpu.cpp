@@ -72,7 +72,8 @@ template <typename F> void Sim::for_worlds(F &&fn) const
 }
 
 Sim::Sim(const mbots_config &cfg)
-    : cfg_(cfg), W_(cfg.num_worlds), cap_(cfg.agent_capacity), A_(cfg.init_num_agents_per_world)
+    : cfg_(cfg), W_(cfg.num_worlds + ((cfg.flags & MBOTS_FLAG_SHARD_GHOST) ? 1u : 0u)), Wx_(cfg.num_worlds),
+      cap_(cfg.agent_capacity), A_(cfg.init_num_agents_per_world)
 {
     const char *e = getenv("MBOTS_CPU_THREADS");
     threads_ = e ? (unsigned)atoi(e) : std::thread::hardware_concurrency();
@@ -332,19 +333,27 @@ void Sim::world_step(uint32_t w, const Table &cur)
 void Sim::scan()
 {
     int32_t tot[kNumSpecies] = {};
-    for (uint32_t w = 0; w < W_; ++w)
+    for (uint32_t w = 0; w < Wx_; ++w)
         for (int s = 0; s < kNumSpecies; ++s) tot[s] += scount_[(size_t)w * kNumSpecies + s];
     int32_t run[kNumSpecies];
     int32_t acc = 0;
     for (int s = 0; s < kNumSpecies; ++s) { run[s] = acc; acc += tot[s]; }
     int32_t off = 0;
-    for (uint32_t w = 0; w < W_; ++w) {
+    for (uint32_t w = 0; w < Wx_; ++w) {
         for (int s = 0; s < kNumSpecies; ++s) {
             row_base_[(size_t)w * kNumSpecies + s] = run[s];
             run[s] += scount_[(size_t)w * kNumSpecies + s];
         }
         world_off_[w] = off;
         off += n_[w];
+    }
+    for (uint32_t w = Wx_; w < W_; ++w) {   // the shard ghost: rows after every exported row
+        int32_t r = acc;
+        for (int s = 0; s < kNumSpecies; ++s) {
+            row_base_[(size_t)w * kNumSpecies + s] = r;
+            r += scount_[(size_t)w * kNumSpecies + s];
+        }
+        world_off_[w] = acc;
     }
     N_ = (uint32_t)acc;
     totals_[0] = N_;
@@ -534,14 +543,14 @@ void Sim::write_synthetic_actions(uint32_t seed, uint32_t step, bool write_hidde
 
 void Sim::sensor_index(int32_t *out) const
 {
-    for (uint32_t w = 0; w < W_; ++w)
+    for (uint32_t w = 0; w < Wx_; ++w)
         for (int i = 0; i < n_[w]; ++i) out[world_off_[w] + i] = obsrow_[(size_t)w * cap_ + i];
 }
 
 uint64_t Sim::overflow() const
 {
     uint64_t s = 0;
-    for (uint32_t v : overflow_) s += v;
+    for (uint32_t w = 0; w < Wx_; ++w) s += overflow_[w];
     return s;
 }
 
@@ -553,7 +562,7 @@ int Sim::export_tensor(int32_t id, mbots_tensor *out)
     int dt = MBOTS_DTYPE_INT32;
     int64_t rows = N_, cols = 1;
     switch (id) {
-    case MBOTS_EXPORT_RESET: p = zeros_worlds_.data(); rows = W_; break;
+    case MBOTS_EXPORT_RESET: p = zeros_worlds_.data(); rows = Wx_; break;
     case MBOTS_EXPORT_ACTION: p = t.action.data(); cols = 6; break;
     case MBOTS_EXPORT_PREV_ACTION: p = t.paction.data(); cols = 6; break;
     case MBOTS_EXPORT_HIDDEN_STATE: p = t.hidden.data(); dt = MBOTS_DTYPE_FLOAT32; cols = kHidden; break;
@@ -576,7 +585,7 @@ int Sim::export_tensor(int32_t id, mbots_tensor *out)
     case MBOTS_EXPORT_STATS: p = t.stats.data(); cols = 4; break;
     case MBOTS_EXPORT_PREV_STATS: p = t.pstats.data(); cols = 4; break;
     case MBOTS_EXPORT_SENSOR_INDEX: sensor_index(sensor_index_.data()); p = sensor_index_.data(); break;
-    case MBOTS_EXPORT_SPECIES_COUNT: p = scount_.data(); rows = W_; cols = kNumSpecies; break;
+    case MBOTS_EXPORT_SPECIES_COUNT: p = scount_.data(); rows = Wx_; cols = kNumSpecies; break;
     case MBOTS_EXPORT_SPECIES: p = t.species.data(); break;
     case MBOTS_EXPORT_PREV_SPECIES: p = t.pspecies.data(); break;
     default: return MBOTS_E_INVALID;

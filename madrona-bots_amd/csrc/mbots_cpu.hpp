@@ -59,7 +59,7 @@ private:
     void sensor_world(uint32_t w, Table &nxt);
 
     mbots_config cfg_;
-    uint32_t W_, cap_, A_;
+    uint32_t W_, Wx_, cap_, A_;   // simulated / exported worlds (W_ = Wx_ + the shard ghost)
     unsigned threads_;
     // agent state, [W][cap] (slot order = creation order, survivors compacted)
     std::vector<float> x_, y_, rw_, rz_, sur0_, sur1_;

@@ -187,9 +187,9 @@ __global__ __launch_bounds__(256, kCap <= 128 ? 8 : 4) void world_step_kernel(Si
     const uint32_t w = uniform(blockIdx.x * kWorldsPerBlock + wv);
     if (w < S.W) world_step(S, cur, lds[wv], w, lane);
     // per-block species/agent counts -> the K2 scan tile (one atomic per counter)
-    if (lane < 5) {
+    if (lane < 5) {   // (a shard ghost, w >= Wx, is not counted: its rows follow the table's)
         const int32_t *sc = lds[wv].scount;
-        blk[wv][lane] = (w < S.W) ? (lane < 4 ? sc[lane] : sc[0] + sc[1] + sc[2] + sc[3]) : 0;
+        blk[wv][lane] = (w < S.Wx) ? (lane < 4 ? sc[lane] : sc[0] + sc[1] + sc[2] + sc[3]) : 0;
     }
     __syncthreads();
     if (threadIdx.x < 5) {
@@ -588,8 +588,16 @@ __global__ __launch_bounds__(1024) void scan_kernel(SimState S, int parity)
         rb.y = s_tot[0] + ex[1];
         rb.z = s_tot[0] + s_tot[1] + ex[2];
         rb.w = s_tot[0] + s_tot[1] + s_tot[2] + ex[3];
+        int32_t off = ex[4];
+        if (w >= S.Wx) {   // the shard ghost: its rows after every exported row
+            rb.x = s_tot[4];
+            rb.y = rb.x + c[0];
+            rb.z = rb.y + c[1];
+            rb.w = rb.z + c[2];
+            off = s_tot[4];
+        }
         reinterpret_cast<int4 *>(S.row_base)[w] = rb;
-        S.world_off[w] = ex[4];
+        S.world_off[w] = off;
     }
     if (t < 5) S.tiles[(size_t)(parity ^ 1) * S.ntiles * 5 + b * 5 + t] = 0;
     if (b == 0 && t == 0) {
@@ -617,7 +625,7 @@ __global__ __launch_bounds__(1024) void tile_sum_kernel(SimState S, int parity)
     const int t = threadIdx.x, b = blockIdx.x;
     const uint32_t w = (uint32_t)b * kTileWorlds + (uint32_t)t;
     int32_t c[5] = {0, 0, 0, 0, 0};
-    if (w < S.W) {
+    if (w < S.Wx) {
         const int4 sc = reinterpret_cast<const int4 *>(S.scount)[w];
         c[0] = sc.x; c[1] = sc.y; c[2] = sc.z; c[3] = sc.w;
         c[4] = sc.x + sc.y + sc.z + sc.w;

@@ -7,6 +7,7 @@ namespace mbots {
 
 constexpr uint32_t kFlagRewardFixed = 0x1u;   // MBOTS_FLAG_REWARD_FIXED
 constexpr uint32_t kFlagFixDepth = 0x2u;      // MBOTS_FLAG_FIX_DEPTH_ALIAS
+constexpr uint32_t kFlagShardGhost = 0x4u;    // MBOTS_FLAG_SHARD_GHOST
 
 // Agent / world state in HBM (SoA).  Agent columns are [W][cap].
 struct SimState {
@@ -39,6 +40,8 @@ struct SimState {
     int32_t *species_out, *obsrow_out, *n_out;
     uint64_t *food_out;
     uint32_t W, cap, A, world_offset, flags, seed, ntiles;
+    uint32_t Wx;                    // exported worlds: W, or W - 1 with the shard ghost (the
+                                    // last world, its rows placed after every exported row)
 };
 
 inline void swap_state(SimState &S)

@@ -159,7 +159,7 @@ void fill_table(mbots::ObsTable &t, Arena &a, size_t rows)
 size_t layout(mbots_handle *h, Arena &a)
 {
     using namespace mbots;
-    const size_t W = h->cfg.num_worlds, cap = h->cfg.agent_capacity, rows = W * cap;
+    const size_t W = h->S.W, cap = h->cfg.agent_capacity, rows = W * cap;
     SimState &S = h->S;
     S.x = a.take<float>(rows);
     S.y = a.take<float>(rows);
@@ -322,7 +322,7 @@ std::vector<Seg> ckpt_segments(mbots_handle *h, mbots::ObsTable &t, uint32_t n_r
 {
     using namespace mbots;
     SimState &S = h->S;
-    const size_t W = h->cfg.num_worlds, rows = W * h->cfg.agent_capacity, N = n_rows;
+    const size_t W = S.W, rows = W * h->cfg.agent_capacity, N = n_rows;
     std::vector<Seg> v = {
         {S.x, rows * 4}, {S.y, rows * 4}, {S.rw, rows * 4}, {S.rz, rows * 4},
         {S.species, rows * 4}, {S.health, rows * 4}, {S.finder, rows * 4}, {S.obsrow, rows * 4},
@@ -398,6 +398,9 @@ int mbots_create(const mbots_config *cfg_in, mbots_handle **out)
     mbots_handle *h = new mbots_handle();
     h->cfg = cfg;
     h->device = cfg.gpu_id;
+    // the shard ghost is one more simulated world (the last), never exported
+    h->S.W = cfg.num_worlds + ((cfg.flags & MBOTS_FLAG_SHARD_GHOST) ? 1u : 0u);
+    h->S.Wx = cfg.num_worlds;
     Arena probe;
     const size_t bytes = layout(h, probe);
     if (hipMalloc(&h->arena.base, bytes) != hipSuccess) {
@@ -408,7 +411,6 @@ int mbots_create(const mbots_config *cfg_in, mbots_handle **out)
     h->arena.used = 0;
     layout(h, h->arena);
     mbots::SimState &S = h->S;
-    S.W = cfg.num_worlds;
     S.cap = cfg.agent_capacity;
     S.A = cfg.init_num_agents_per_world;
     S.world_offset = cfg.world_offset;
@@ -902,7 +904,7 @@ int mbots_load_checkpoint(mbots_handle *h, const void *src, uint64_t bytes)
         hd.A != h->cfg.init_num_agents_per_world || hd.world_offset != h->cfg.world_offset ||
         hd.flags != h->cfg.flags || hd.seed != h->cfg.rand_seed)
         return fail(MBOTS_E_INVALID, "checkpoint configuration differs from the manager's");
-    if (hd.n_rows > (uint64_t)h->cfg.num_worlds * h->cfg.agent_capacity)
+    if (hd.n_rows > (uint64_t)h->S.W * h->cfg.agent_capacity)
         return fail(MBOTS_E_INVALID, "checkpoint row count out of range");
     HIP_TRY(hipSetDevice(h->device));
     HIP_TRY(hipDeviceSynchronize());

@@ -105,6 +105,7 @@ _DTYPES = {0: (torch.uint8, "|u1"), 1: (torch.int8, "|i1"), 2: (torch.int32, "<i
 
 FLAG_REWARD_FIXED = 0x1
 FLAG_FIX_DEPTH_ALIAS = 0x2
+FLAG_SHARD_GHOST = 0x4
 
 
 class ExecMode:
@@ -190,17 +191,20 @@ class SimManager:
     (per-world slot cap), world_offset (global index of this shard's first
     world), reward_fixed (rewards[speciesID-1] instead of the reference's
     off-by-one), fix_depth_alias (depth_tensor returns real depth,
-    SURVEY B.1)."""
+    SURVEY B.1), shard_ghost (also step world world_offset + num_worlds, never
+    exported, so a shard's faithful B.3 rewards equal one device's; its agents
+    act on the write_synthetic_actions stream)."""
 
     def __init__(self, gpu_id, num_worlds, rand_seed, init_num_agents_per_world, *,
                  exec_mode="hip", agent_capacity=128, world_offset=0, reward_fixed=False,
-                 fix_depth_alias=False):
+                 fix_depth_alias=False, shard_ghost=False):
         self.exec_mode = _exec_mode(exec_mode)
         self.gpu_id = int(gpu_id)
         self.num_worlds = int(num_worlds)
         self.agent_capacity = int(agent_capacity)
         flags = (FLAG_REWARD_FIXED if reward_fixed else 0) | \
-                (FLAG_FIX_DEPTH_ALIAS if fix_depth_alias else 0)
+                (FLAG_FIX_DEPTH_ALIAS if fix_depth_alias else 0) | \
+                (FLAG_SHARD_GHOST if shard_ghost else 0)
         cfg = _Config(self.gpu_id, self.num_worlds, int(rand_seed) & 0xFFFFFFFF,
                       int(init_num_agents_per_world), 32, int(world_offset),
                       int(agent_capacity), flags, self.exec_mode)

@@ -72,10 +72,13 @@ def _segments(counts):
 
 
 @pytest.mark.timeout(600)
-def test_config4_eight_shards_equal_one_manager():
+@pytest.mark.parametrize("reward_fixed", [True, False])
+def test_config4_eight_shards_equal_one_manager(reward_fixed):
     """262144 worlds = 8 x 32768 (world_offset = r * 32768) on one device vs one
     262144-world manager: per species, the full table's segment is the
-    concatenation of the shards' segments (rows (species, world, slot))."""
+    concatenation of the shards' segments (rows (species, world, slot)).  In
+    the faithful B.3 mode shards 0..6 step a ghost of the next shard's first
+    world (shard_ghost), as bench.py's ranks do."""
     import madrona_bots as mb
     R, WS = 8, 32768
     steps = 5
@@ -90,11 +93,12 @@ def test_config4_eight_shards_equal_one_manager():
             m.shift_observations()
         torch.cuda.synchronize()
 
-    full = mb.SimManager(0, R * WS, 69, 32, reward_fixed=True)
+    full = mb.SimManager(0, R * WS, 69, 32, reward_fixed=reward_fixed)
     run(full)
     shards = []
     for r in range(R):
-        s = mb.SimManager(0, WS, 69, 32, reward_fixed=True, world_offset=r * WS)
+        s = mb.SimManager(0, WS, 69, 32, reward_fixed=reward_fixed, world_offset=r * WS,
+                          shard_ghost=(not reward_fixed) and r < R - 1)
         run(s)
         shards.append(s)
     fcnt = full.species_count_tensor().to_torch().cpu().numpy()
