@@ -89,8 +89,9 @@ struct mbots_handle {
     bool six_lazy[2] = {false, false};
     bool prev_lazy[2] = {false, false};   // table half's six shift-owned Prev* columns are
                                           // still its current ones (lazy shift, K5)
-    int forced = 0;                   // deferred parts the caller's reads forced since the
+    int forced = 0;                   // deferred parts the caller's reads needed since the
                                       // last step (kMove*): the next step prefetches them
+    int prefetched = 0;               // parts this step prefetched and no shift superseded
     uint64_t steps = 0;               // steps run
     hipStream_t last_stream = nullptr;
     bool timing = false;
@@ -285,6 +286,13 @@ int pending_mask(const mbots_handle *h)
     const int tb = h->tb;
     return (h->cur_ah_pending[tb] ? mbots::kMoveAH : 0) | (h->psem_pending[tb] ? mbots::kMoveSensor : 0) |
            (h->ah_pending[tb] ? mbots::kMovePrevAH : 0) | (h->six_pending[tb] ? mbots::kMovePrev6 : 0);
+}
+
+// a caller's read that needs the parts `need`: the ones the step deferred
+// (owed when the read came) or prefetched are remembered for the next step
+void note_use(mbots_handle *h, int need, int owed)
+{
+    h->forced |= need & (owed | h->prefetched);
 }
 
 int sync_totals(mbots_handle *h)
@@ -524,6 +532,7 @@ int mbots_step(mbots_handle *h, void *stream)
     const int prefetch = h->forced;
 #endif
     h->forced = 0;
+    h->prefetched = prefetch;
     // no shift since the last step: its deferred Prev moves first
     if (h->six_pending[h->tb] && (rc = materialize_prev(h, st))) return rc;
     if ((rc = materialize_prev_ah(h, st))) return rc;
@@ -612,6 +621,9 @@ int mbots_shift_observations(mbots_handle *h, void *stream)
                      : mbots::launch_shift(h->S, h->T[h->tb], mbots::kShiftEager, st);
     });
     if (rc == MBOTS_OK) {
+        // Action / HiddenState and every Prev* column but the sensor's are the
+        // shift's now: a later read of them is not the step's deferred move
+        h->prefetched &= mbots::kMoveSensor;
         h->cur_ah_pending[h->tb] = false;
         if (with_psem) h->psem_pending[h->tb] = false;
         h->prev_lazy[h->tb] = true;
@@ -646,23 +658,28 @@ int mbots_export(mbots_handle *h, int32_t id, mbots_tensor *out)
     int rc = mbots_num_agents(h, &N);
     if (rc) return rc;
     const int owed = pending_mask(h);
+    int need = 0;
     switch (id) {
     case MBOTS_EXPORT_PREV_SPECIES: case MBOTS_EXPORT_PREV_POSITION: case MBOTS_EXPORT_PREV_HEALTH:
     case MBOTS_EXPORT_PREV_SURROUNDING: case MBOTS_EXPORT_PREV_REWARD: case MBOTS_EXPORT_PREV_STATS:
+        need = mbots::kMovePrev6;
         if ((rc = materialize_prev(h, h->last_stream))) return rc;
         break;
     case MBOTS_EXPORT_PREV_ACTION: case MBOTS_EXPORT_PREV_HIDDEN_STATE:
+        need = mbots::kMovePrevAH;
         if ((rc = materialize_prev_ah(h, h->last_stream))) return rc;
         break;
     case MBOTS_EXPORT_ACTION: case MBOTS_EXPORT_HIDDEN_STATE:
+        need = mbots::kMoveAH;
         if ((rc = materialize_cur_ah(h, h->last_stream))) return rc;
         break;
     case MBOTS_EXPORT_PREV_SENSOR_SEMANTIC: case MBOTS_EXPORT_PREV_SENSOR_DEPTH:
+        need = mbots::kMoveSensor;
         if ((rc = materialize_psem(h, h->last_stream))) return rc;
         break;
     default: break;
     }
-    h->forced |= owed & ~pending_mask(h);
+    note_use(h, need, owed);
     const ObsTable &t = h->T[h->tb];
     const bool fixd = (h->cfg.flags & MBOTS_FLAG_FIX_DEPTH_ALIAS) != 0;
     void *p = nullptr;
@@ -729,7 +746,7 @@ int mbots_set_action(mbots_handle *h, uint32_t row, const int32_t action[6])
     }
     const int owed = pending_mask(h);
     if ((rc = materialize_cur_ah(h, h->last_stream))) return rc;
-    h->forced |= owed & ~pending_mask(h);
+    note_use(h, mbots::kMoveAH, owed);
     HIP_TRY(hipMemcpyAsync(h->T[h->tb].action + (size_t)row * 6, action, 6 * sizeof(int32_t),
                            hipMemcpyHostToDevice, h->last_stream));
     HIP_TRY(hipStreamSynchronize(h->last_stream));
@@ -766,7 +783,7 @@ int mbots_write_synthetic_actions(mbots_handle *h, uint32_t seed, uint32_t step,
     const int owed = pending_mask(h);
     int rc = materialize_cur_ah(h, st);
     if (rc) return rc;
-    h->forced |= owed & ~pending_mask(h);
+    note_use(h, mbots::kMoveAH, owed);
     return timed(h, MBOTS_TK_ACTIONS, st, [&] {
         return mbots::launch_synthetic_actions(h->S, h->T[h->tb], seed, step, write_hidden, st);
     });
@@ -788,7 +805,7 @@ int mbots_construct_obs(mbots_handle *h, int32_t prev, float *out, uint64_t out_
     if (!prev && (rc = wait_sensor(h))) return rc;   // current semantic rows come from K3b
     if (prev && h->six_pending[h->tb] && (rc = materialize_prev(h, st))) return rc;
     if (prev && (rc = materialize_psem(h, st))) return rc;
-    h->forced |= owed & ~pending_mask(h);
+    if (prev) note_use(h, mbots::kMovePrev6 | mbots::kMoveSensor, owed);
     return timed(h, MBOTS_TK_OBS, st, [&] {
         return mbots::launch_construct_obs(h->S, h->T[h->tb], prev, h->prev_lazy[h->tb] ? 1 : 0, out,
                                            (uint32_t)out_rows, st);
@@ -926,6 +943,7 @@ int mbots_load_checkpoint(mbots_handle *h, const void *src, uint64_t bytes)
     h->cur_ah_pending[0] = h->cur_ah_pending[1] = false;
     h->psem_pending[0] = h->psem_pending[1] = false;
     h->forced = 0;
+    h->prefetched = 0;
     h->steps = 1;
     hipStream_t st = nullptr;
     int rc = record_totals(h, st);
