@@ -821,13 +821,11 @@ constexpr int kQueueCap = 128;                // P1 survivors (flushed at >= 64)
 constexpr float kWedge = 1.41421356f + 0.05f; // |l| <= |f| + sqrt(2): necessary for |u| < 1
 constexpr float kUEps = 2e-3f;                // root-interval margin in u
 // food squares lie inside their circumscribed circle, radius sqrt 2 (1.42 with
-// margin): the wedge |l| <= |f| + sqrt(2) 1.42, candidate pixels from that
-// circle's roots when |f| > kFoodFar (the square then lies wholly on one side
-// of the camera plane), at most kFoodInline candidates tested inline
-constexpr float kFoodR2 = 1.42f * 1.42f;
+// margin): the wedge |l| <= |f| + sqrt(2) 1.42; candidate pixels from the
+// corner slopes when |f| > kFoodFar (the square then lies wholly on one side
+// of the camera plane), every ray exactly (the wide list) otherwise
 constexpr float kWedgeFood = 1.41421356f * 1.42f + 0.05f;
 constexpr float kFoodFar = 2.5f;
-constexpr int kFoodInline = 6;
 constexpr float kFarCull = 5.0f;               // P1 angular cull from this |f| on
 
 template <int kCap>
@@ -900,8 +898,9 @@ __device__ __forceinline__ void run_wide(LDS &L, int nf, int a0, int q0, int cnt
     }
 }
 
-// P2: survivors [q0, q0 + cnt): approximate roots bound the candidate pixels;
-// <= 2 pixels + the finder are tested inline, wider pairs go to the wide list
+// P2: survivors [q0, q0 + cnt): the approximate hit interval bounds the
+// candidate pixels; the edge pixels and the finder get the exact test inline,
+// near pairs go to the wide list
 template <class LDS>
 __device__ __forceinline__ void run_survivors(LDS &L, int nf, int a0, int q0, int cnt)
 {
@@ -919,53 +918,69 @@ __device__ __forceinline__ void run_survivors(LDS &L, int nf, int a0, int q0, in
         if (food ? fabsf(f) <= kFoodFar : (r2 <= 1.0f) | (fabsf(f) <= 1.5f)) {
             wide = true;
         } else {
+            // A far pair: the object lies wholly on one side of the camera
+            // plane (circle: |f| > 1.5; square: |f| > 2.5 > its half-diagonal
+            // 1.42, so every corner has |X| >= 1.08).  Its hit interval in u,
+            // approximately: the circle's roots (lf -+ sqrt(r^2 - 1)) / (f^2 - 1),
+            // or the square's extreme corner slopes Y / X.
             const bool fwd = f > 0.0f;
-            // bounding circle: radius 1 (agents) / 1.42 (food squares)
-            const float R2 = food ? kFoodR2 : 1.0f;
-            const float sq = __builtin_amdgcn_sqrtf(food ? R2 * (r2 - R2) : r2 - 1.0f);
-            const float lf = l * f;
-            // approximate roots u = (lf -+ R sqrt(r^2 - R^2)) / (f^2 - R^2), widened by kUEps, in
-            // pixel coordinates s = (u + 1) sc - 0.5 (pixel k at s = k)
             const float sc = fwd ? 12.0f : 4.0f;
-            const float sia = sc * __builtin_amdgcn_rcpf(f * f - R2);
-            // (FMA: an approximation bounded by the kUEps margin either way)
-            const float lo = __builtin_fmaf(lf - sq, sia, fwd ? 12.0f * (1.0f - kUEps) - 0.5f : 4.0f * (1.0f - kUEps) - 0.5f);
-            const float hi = __builtin_fmaf(lf + sq, sia, fwd ? 12.0f * (1.0f + kUEps) - 0.5f : 4.0f * (1.0f + kUEps) - 0.5f);
+            float ulo, uhi;
+            FoodBox b{};
+            if (food) {
+                b = box_setup(f, l, L.frot[j], L.hd[a0 + ic]);
+                // corner offsets +-(p - q, p + q), +-(p + q, q - p)
+                const float ax = b.p - b.q, ay = b.p + b.q;
+                const float s0 = (l + ay) * __builtin_amdgcn_rcpf(f + ax);
+                const float s1 = (l - ay) * __builtin_amdgcn_rcpf(f - ax);
+                const float s2 = (l - ax) * __builtin_amdgcn_rcpf(f + ay);
+                const float s3 = (l + ax) * __builtin_amdgcn_rcpf(f - ay);
+                ulo = fminf(fminf(s0, s1), fminf(s2, s3));
+                uhi = fmaxf(fmaxf(s0, s1), fmaxf(s2, s3));
+            } else {
+                const float sq = __builtin_amdgcn_sqrtf(r2 - 1.0f);
+                const float ia = __builtin_amdgcn_rcpf(f * f - 1.0f);
+                const float lf = l * f;
+                ulo = (lf - sq) * ia;
+                uhi = (lf + sq) * ia;
+            }
+            // widened by kUEps, in pixel coordinates s = (u + 1) sc - 0.5
+            // (pixel k at s = k; FMA: an approximation bounded by the margin)
+            const float lo = __builtin_fmaf(ulo, sc, fwd ? 12.0f * (1.0f - kUEps) - 0.5f : 4.0f * (1.0f - kUEps) - 0.5f);
+            const float hi = __builtin_fmaf(uhi, sc, fwd ? 12.0f * (1.0f + kUEps) - 0.5f : 4.0f * (1.0f + kUEps) - 0.5f);
             const int kmax = fwd ? 23 : 7;
             int k0 = max((int)ceilf(lo), 0);
             const int k1 = min((int)floorf(hi), kmax);
             const int c = k1 - k0 + 1;
             k0 += fwd ? 0 : 24;
             uint32_t *kr = L.key + ic * kKeyStride;
-            if (food) {
-                if (c > kFoodInline) {
-                    wide = true;
-                } else {
-                    // every candidate gets the exact test; a far square lies
-                    // wholly on its camera's side, so box_hit is the line test
-                    const FoodBox b = box_setup(f, l, L.frot[j], L.hd[a0 + ic]);
-                    const uint32_t kin = zkey(box_z(b, fwd), order);
-                    for (int k = k0; k < k0 + c; ++k)
-                        if (box_line_hit(b, L.u[k & 31])) atomicMin(&kr[k], kin);
-                    if (fwd & box_line_hit(b, 0.0f)) atomicMin(&kr[kSensor], kin);
-                }
+            // The two edge pixels of [k0, k0 + c) get the exact predicate.
+            // Interior pixels lie >= one pixel pitch minus 2 kUEps (>= 0.08 in
+            // u) inside the true interval, where the approximate bounds are off
+            // by ~1e-6: for a circle the float q(u) is then off by < 1e-4 of a
+            // value <= -0.08; for a square every corner's S = Y - u X is
+            // >= 1.08 x 0.08 from 0 (|X| >= 1.08), against a float error of the
+            // line test < 1e-4.  They are hits carrying the object's key.
+            const int kl = k0 + max(c - 1, 0);
+            const float ua = L.u[k0 & 31], ub = L.u[kl & 31];
+            bool ha, hb, hf;
+            uint32_t kin;
+            if (food) {   // a far square: box_hit is the line test on its side
+                ha = box_line_hit(b, ua);
+                hb = box_line_hit(b, ub);
+                hf = fwd & box_line_hit(b, 0.0f);
+                kin = zkey(box_z(b, fwd), order);
             } else {
-                // the two edge pixels of [k0, k0 + c) get the exact predicate;
-                // interior pixels lie >= one pixel pitch minus kUEps (>= 0.08 in
-                // u) inside the root interval of a pair with r > 1, |f| > 1.5,
-                // where the approximate roots are off by ~1e-6 and the float
-                // q(u) by < 1e-4: they are hits carrying the object's key
-                const int kl = k0 + max(c - 1, 0);
-                const float ua = L.u[k0 & 31], ub = L.u[kl & 31];
-                const uint32_t kin = zkey(fwd ? f - 1.0f : -f - 1.0f, order);
-                const bool ha = far_pixel_hit(f, l, ua, fwd), hb = far_pixel_hit(f, l, ub, fwd);
+                ha = far_pixel_hit(f, l, ua, fwd);
+                hb = far_pixel_hit(f, l, ub, fwd);
                 // finder ray (u = 0) of a far pair: q(0) = l^2 - 1 <= 0 and f > 0
-                const bool hf = (l * l - 1.0f <= 0.0f) & fwd;
-                if ((c > 0) & ha) atomicMin(&kr[k0], kin);
-                if ((c > 1) & hb) atomicMin(&kr[kl], kin);
-                if (hf) atomicMin(&kr[kSensor], kin);
-                for (int k = k0 + 1; k < kl; ++k) atomicMin(&kr[k], kin);
+                hf = (l * l - 1.0f <= 0.0f) & fwd;
+                kin = zkey(fwd ? f - 1.0f : -f - 1.0f, order);
             }
+            if ((c > 0) & ha) atomicMin(&kr[k0], kin);
+            if ((c > 1) & hb) atomicMin(&kr[kl], kin);
+            if (hf) atomicMin(&kr[kSensor], kin);
+            for (int k = k0 + 1; k < kl; ++k) atomicMin(&kr[k], kin);
         }
     }
     // every lane read its code above: the wide ones compact in place

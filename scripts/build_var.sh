@@ -8,6 +8,6 @@ d=$ROOT/build_var/src_$name
 mkdir -p $d
 cp "$src" $d/mbots_kernels.hip
 cp $ROOT/madrona-bots_amd/csrc/{mbots_manager.cpp,mbots_cpu.cpp,mbots_cpu.hpp,mbots_device.hpp,mbots_kernels.hpp,mbots_ray.hpp} $d/
-(cd $d && /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off "$@" \
+(cd $d && /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-slp-vectorize "$@" \
     -shared -o $ROOT/build_var/libmbots_$name.so mbots_kernels.hip mbots_manager.cpp mbots_cpu.cpp)
 rm -rf $d
