@@ -160,6 +160,11 @@ int mbots_world_state(mbots_handle *h, uint32_t world, float *xy_rwrz, int32_t *
  * hidden state gets hash-derived floats when write_hidden != 0. */
 int mbots_write_synthetic_actions(mbots_handle *h, uint32_t seed, uint32_t step,
                                   int32_t write_hidden, void *stream);
+/* Make `stream` wait for this manager's outstanding work on its internal
+ * stream (the last step's sensor).  Every accessor that needs the sensor rows
+ * does this itself; a caller recording steps into a HIP graph (stream capture)
+ * ends the captured sequence with it, so the capture has no unjoined work. */
+int mbots_join(mbots_handle *h, void *stream);
 /* running total of agent-steps (sum over steps of live agents after the step) */
 int mbots_agent_steps(mbots_handle *h, uint64_t *out);
 /* births/respawns dropped because a world reached agent_capacity */

@@ -1450,10 +1450,18 @@ hipError_t launch_world_step(const SimState &S, const ObsTable &cur, int parity,
         hipLaunchKernelGGL(world_step_kernel<256>, dim3(world_blocks(S.W)), dim3(256), 0, st, S, cur, parity);
     return hipGetLastError();
 }
-hipError_t launch_scan(const SimState &S, int parity, hipStream_t st, hipEvent_t done)
+hipError_t launch_scan(const SimState &S, int parity, hipStream_t st, hipEvent_t done, bool plain_events)
 {
     // `done` rides on the dispatch packet itself (no marker packet between K2
     // and the next kernel on this stream)
+    if (!done) {
+        hipLaunchKernelGGL(scan_kernel, dim3(S.ntiles), dim3(1024), 0, st, S, parity);
+        return hipGetLastError();
+    }
+    if (plain_events) {   // stream capture: a capturable event record after the dispatch
+        hipLaunchKernelGGL(scan_kernel, dim3(S.ntiles), dim3(1024), 0, st, S, parity);
+        return hipEventRecord(done, st);
+    }
     hipExtLaunchKernelGGL(scan_kernel, dim3(S.ntiles), dim3(1024), 0, st, nullptr, done, 0u, S, parity);
     return hipGetLastError();
 }
@@ -1509,26 +1517,41 @@ hipError_t launch_move(const SimState &S, const ObsTable &cur, const ObsTable &n
         hipLaunchKernelGGL(move_kernel, dim3(bx, k), dim3(256), 0, st, S.totals, S.src_of, m);
     return hipGetLastError();
 }
+// a dispatch whose completion records `done`: carried by the dispatch packet
+// itself (no marker packet), or -- while the stream is being captured into a
+// graph, where only event records are capturable -- an event record after it
+#define MB_LAUNCH_EV(kern, grid, blk, st, done, plain, ...)                                   \
+    do {                                                                                    \
+        if (plain || !(done)) {                                                             \
+            hipLaunchKernelGGL(kern, grid, blk, 0, st, __VA_ARGS__);                        \
+            if (done) (void)hipEventRecord(done, st);                                       \
+        } else {                                                                            \
+            hipExtLaunchKernelGGL(kern, grid, blk, 0u, st, nullptr, done, 0u, __VA_ARGS__); \
+        }                                                                                   \
+    } while (0)
+
 template <int kCap>
-static void launch_sensor_cap(const SimState &S, const ObsTable &nxt, hipStream_t st, hipEvent_t done)
+static void launch_sensor_cap(const SimState &S, const ObsTable &nxt, hipStream_t st, hipEvent_t done,
+                              bool plain_events)
 {
     const bool fixd = (S.flags & kFlagFixDepth) != 0;
     const dim3 blk(64 * kSensorWorlds);
     if (S.W <= (uint32_t)MB_SENSOR_SPLIT_MAX) {   // small: MB_SENSOR_SPLIT waves per world
         constexpr int kWpb = kSensorWorlds / MB_SENSOR_SPLIT;
         const dim3 grid((S.W + kWpb - 1) / kWpb);
-        if (fixd) hipExtLaunchKernelGGL((sensor_kernel<true, MB_SENSOR_SPLIT, kCap>), grid, blk, 0u, st, nullptr, done, 0u, S, nxt);
-        else hipExtLaunchKernelGGL((sensor_kernel<false, MB_SENSOR_SPLIT, kCap>), grid, blk, 0u, st, nullptr, done, 0u, S, nxt);
+        if (fixd) MB_LAUNCH_EV((sensor_kernel<true, MB_SENSOR_SPLIT, kCap>), grid, blk, st, done, plain_events, S, nxt);
+        else MB_LAUNCH_EV((sensor_kernel<false, MB_SENSOR_SPLIT, kCap>), grid, blk, st, done, plain_events, S, nxt);
     } else {
         const dim3 grid((S.W + kSensorWorlds - 1) / kSensorWorlds);
-        if (fixd) hipExtLaunchKernelGGL((sensor_kernel<true, 1, kCap>), grid, blk, 0u, st, nullptr, done, 0u, S, nxt);
-        else hipExtLaunchKernelGGL((sensor_kernel<false, 1, kCap>), grid, blk, 0u, st, nullptr, done, 0u, S, nxt);
+        if (fixd) MB_LAUNCH_EV((sensor_kernel<true, 1, kCap>), grid, blk, st, done, plain_events, S, nxt);
+        else MB_LAUNCH_EV((sensor_kernel<false, 1, kCap>), grid, blk, st, done, plain_events, S, nxt);
     }
 }
-hipError_t launch_sensor(const SimState &S, const ObsTable &nxt, hipStream_t st, hipEvent_t done)
+hipError_t launch_sensor(const SimState &S, const ObsTable &nxt, hipStream_t st, hipEvent_t done,
+                         bool plain_events)
 {
-    if (S.cap <= 128) launch_sensor_cap<128>(S, nxt, st, done);
-    else launch_sensor_cap<256>(S, nxt, st, done);
+    if (S.cap <= 128) launch_sensor_cap<128>(S, nxt, st, done, plain_events);
+    else launch_sensor_cap<256>(S, nxt, st, done, plain_events);
     return hipGetLastError();
 }
 hipError_t launch_shift(const SimState &S, const ObsTable &t, int mode, hipStream_t st)

@@ -65,7 +65,9 @@ uint32_t scan_tiles(uint32_t W);
 hipError_t launch_init(const SimState &S, hipStream_t st);
 hipError_t launch_tile_sum(const SimState &S, int parity, hipStream_t st);
 hipError_t launch_world_step(const SimState &S, const ObsTable &cur, int parity, hipStream_t st);
-hipError_t launch_scan(const SimState &S, int parity, hipStream_t st, hipEvent_t done = nullptr);
+// plain_events: record `done` with hipEventRecord (stream capture) instead of on the dispatch
+hipError_t launch_scan(const SimState &S, int parity, hipStream_t st, hipEvent_t done = nullptr,
+                       bool plain_events = false);
 hipError_t launch_export_rows(const SimState &S, const ObsTable &nxt, int init, hipStream_t st);
 // K4 parts (DESIGN.md "Deferred Prev moves"): Action + HiddenState; the same
 // also into PrevAction / PrevHiddenState (the fused shift); the prev sensor;
@@ -75,7 +77,7 @@ constexpr int kMoveAll = kMoveAH | kMoveSensor | kMovePrevAH | kMovePrev6;
 hipError_t launch_move(const SimState &S, const ObsTable &cur, const ObsTable &nxt, int prev_lazy,
                        int parts, hipStream_t st);
 hipError_t launch_sensor(const SimState &S, const ObsTable &nxt, hipStream_t st,
-                         hipEvent_t done = nullptr);
+                         hipEvent_t done = nullptr, bool plain_events = false);
 // shift modes: every Prev* column / Action + HiddenState only (lazy) / the six
 // columns a lazy shift left (materialise)
 constexpr int kShiftAll = 0, kShiftEager = 1, kShiftRest = 2;

@@ -79,6 +79,7 @@ struct mbots_handle {
     hipStream_t aux = nullptr;        // internal stream of the K3b sensor (forked after K2)
     hipEvent_t ev_join[2] = {nullptr, nullptr};   // K3b of alternate steps done (aux)
     int last_join = -1;               // ev_join of the latest K3b, -1: none pending
+    unsigned long long join_capture = 0;   // stream-capture id it was recorded in (0: none)
     // deferred K4 parts of a table half (moved from the other half along the
     // last src_of when needed): PrevAction / PrevHiddenState, the six other
     // Prev* columns (from the other half's current ones when six_lazy)
@@ -540,14 +541,24 @@ int mbots_step(mbots_handle *h, void *stream)
     if ((rc = materialize_psem(h, st))) return rc;   // before this step's sensor rewrites its source
     // K1 reads the finder slots the previous step's sensor wrote, and writes the
     // state half that sensor read; the halves swap after K1.
-    if (h->last_join >= 0) HIP_TRY(hipStreamWaitEvent(st, h->ev_join[h->last_join], 0));
+    // (under stream capture only a join recorded in the same capture is waited
+    // for: a replay starts after the previous launch of the graph completed)
+    hipStreamCaptureStatus cap_status = hipStreamCaptureStatusNone;
+    unsigned long long cap_id = 0;
+    HIP_TRY(hipStreamGetCaptureInfo(st, &cap_status, &cap_id));
+    const bool capturing = cap_status == hipStreamCaptureStatusActive;
+    if (h->last_join >= 0 && (!capturing || h->join_capture == cap_id))
+        HIP_TRY(hipStreamWaitEvent(st, h->ev_join[h->last_join], 0));
     if ((rc = timed(h, MBOTS_TK_WORLD_STEP, st,
                     [&] { return mbots::launch_world_step(h->S, cur, par, st); })))
         return rc;
     mbots::swap_state(h->S);
     // K2 writes the row counts into the pinned mirror; accessors and the
     // sensor's stream wait on ev_totals, carried by K2's own dispatch
-    if ((rc = timed(h, MBOTS_TK_SCAN, st, [&] { return mbots::launch_scan(h->S, par, st, h->ev_totals); })))
+    // (under stream capture -- a caller recording steps into a HIP graph -- the
+    // fork / join events are recorded by hipEventRecord, the capturable form)
+    if ((rc = timed(h, MBOTS_TK_SCAN, st,
+                    [&] { return mbots::launch_scan(h->S, par, st, h->ev_totals, capturing); })))
         return rc;
 #ifdef MB_NO_FORK
     if ((rc = timed(h, MBOTS_TK_EXPORT, st,
@@ -567,9 +578,10 @@ int mbots_step(mbots_handle *h, void *stream)
     const int jcur = h->last_join == 0 ? 1 : 0;
     HIP_TRY(hipStreamWaitEvent(h->aux, h->ev_totals, 0));
     if ((rc = timed(h, MBOTS_TK_SENSOR, h->aux,
-                    [&] { return mbots::launch_sensor(h->S, nxt, h->aux, h->ev_join[jcur]); })))
+                    [&] { return mbots::launch_sensor(h->S, nxt, h->aux, h->ev_join[jcur], capturing); })))
         return rc;
     h->last_join = jcur;
+    h->join_capture = capturing ? cap_id : 0;
     if ((rc = timed(h, MBOTS_TK_EXPORT, st,
                     [&] { return mbots::launch_export_rows(h->S, nxt, 0, st); })))
         return rc;
@@ -810,6 +822,15 @@ int mbots_construct_obs(mbots_handle *h, int32_t prev, float *out, uint64_t out_
         return mbots::launch_construct_obs(h->S, h->T[h->tb], prev, h->prev_lazy[h->tb] ? 1 : 0, out,
                                            (uint32_t)out_rows, st);
     });
+}
+
+int mbots_join(mbots_handle *h, void *stream)
+{
+    if (!h) return fail(MBOTS_E_INVALID, "null handle");
+    if (h->cpu) return MBOTS_OK;   // synchronous: nothing outstanding
+    HIP_TRY(hipSetDevice(h->device));
+    if (h->last_join >= 0) HIP_TRY(hipStreamWaitEvent(as_stream(stream), h->ev_join[h->last_join], 0));
+    return MBOTS_OK;
 }
 
 int mbots_agent_steps(mbots_handle *h, uint64_t *out)

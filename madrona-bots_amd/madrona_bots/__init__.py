@@ -68,6 +68,7 @@ def _load():
         "mbots_set_action": [vp, u32, P(i32)],
         "mbots_agent_offset_for_world": [vp, u32, P(u32)],
         "mbots_write_synthetic_actions": [vp, u32, u32, i32, vp],
+        "mbots_join": [vp, vp],
         "mbots_agent_steps": [vp, P(ctypes.c_uint64)],
         "mbots_overflow": [vp, P(ctypes.c_uint64)],
         "mbots_enable_kernel_timing": [vp, i32],
@@ -377,6 +378,12 @@ class SimManager:
                 arrays[f"w{int(w)}/{k}"] = v
         np.savez(path, **arrays)
         return sorted(arrays)
+
+    def join(self):
+        """Make torch's current stream wait for the manager's outstanding
+        sensor work (mbots_join): ends a sequence of steps captured into a
+        HIP graph (torch.cuda.graph) with no unjoined work."""
+        _check(_lib.mbots_join(self._h, self._stream()))
 
     def write_synthetic_actions(self, seed, step, write_hidden=False):
         _check(_lib.mbots_write_synthetic_actions(self._h, int(seed) & 0xFFFFFFFF,
