@@ -176,27 +176,42 @@ template <int kCap>
 __device__ void world_step(SimState &S, const ObsTable &cur, WorldLDS<kCap> &L, uint32_t w,
                            uint32_t lane);
 
+#ifndef MB_K1_WPB
+#define MB_K1_WPB 4
+#endif
+constexpr int kK1Worlds = MB_K1_WPB;          // worlds (waves) per K1 block
 template <int kCap>
-__global__ __launch_bounds__(256, kCap <= 128 ? 8 : 4) void world_step_kernel(SimState S, ObsTable cur,
-                                                                              int parity)
+__global__ __launch_bounds__(64 * kK1Worlds, (kCap <= 128 ? 32 : 16) / kK1Worlds) void world_step_kernel(
+    SimState S, ObsTable cur, int parity)
 {
-    __shared__ WorldLDS<kCap> lds[kWorldsPerBlock];
-    __shared__ int32_t blk[kWorldsPerBlock][5];
+    __shared__ WorldLDS<kCap> lds[kK1Worlds];
     const uint32_t wv = threadIdx.x >> 6;
     const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t w = uniform(blockIdx.x * kWorldsPerBlock + wv);
+    const uint32_t w = uniform(blockIdx.x * kK1Worlds + wv);
     if (w < S.W) world_step(S, cur, lds[wv], w, lane);
-    // per-block species/agent counts -> the K2 scan tile (one atomic per counter)
-    if (lane < 5) {   // (a shard ghost, w >= Wx, is not counted: its rows follow the table's)
-        const int32_t *sc = lds[wv].scount;
-        blk[wv][lane] = (w < S.Wx) ? (lane < 4 ? sc[lane] : sc[0] + sc[1] + sc[2] + sc[3]) : 0;
-    }
-    __syncthreads();
-    if (threadIdx.x < 5) {
-        const int32_t v = blk[0][threadIdx.x] + blk[1][threadIdx.x] + blk[2][threadIdx.x] +
-                          blk[3][threadIdx.x];
-        const uint32_t tile = (blockIdx.x * kWorldsPerBlock) / kTileWorlds;
-        atomicAdd(&S.tiles[(size_t)parity * S.ntiles * 5 + tile * 5 + threadIdx.x], v);
+    int32_t *tiles = S.tiles + (size_t)parity * S.ntiles * 5;
+    if constexpr (kK1Worlds == 1) {
+        // one world per block: its species/agent counts go straight to the K2
+        // scan tile (no block barrier: a block's LDS frees as its world ends)
+        if (w < S.Wx && lane < 5) {   // (a shard ghost, w >= Wx, is not counted)
+            const int32_t *sc = lds[0].scount;
+            atomicAdd(&tiles[(w / kTileWorlds) * 5 + lane], lane < 4 ? sc[lane] : sc[0] + sc[1] + sc[2] + sc[3]);
+        }
+    } else {
+        __shared__ int32_t blk[kK1Worlds][5];
+        // per-block species/agent counts -> the K2 scan tile (one atomic per counter)
+        if (lane < 5) {   // (a shard ghost, w >= Wx, is not counted: its rows follow the table's)
+            const int32_t *sc = lds[wv].scount;
+            blk[wv][lane] = (w < S.Wx) ? (lane < 4 ? sc[lane] : sc[0] + sc[1] + sc[2] + sc[3]) : 0;
+        }
+        __syncthreads();
+        if (threadIdx.x < 5) {
+            int32_t v = 0;
+#pragma unroll
+            for (int k = 0; k < kK1Worlds; ++k) v += blk[k][threadIdx.x];
+            const uint32_t tile = (blockIdx.x * kK1Worlds) / kTileWorlds;
+            atomicAdd(&tiles[tile * 5 + threadIdx.x], v);
+        }
     }
 }
 
@@ -225,9 +240,13 @@ __device__ void world_step(SimState &S, const ObsTable &cur, WorldLDS<kCap> &L, 
     {
         // slots < min(n0, 64) (n0 is one scalar load; the first wave round is
         // bandwidth-bound, so the ~half of the lanes past n0 stay idle: K1 -2.4 %)
+        // -- except the export rows, loaded for every lane beside n0 so that the
+        // action rows they point at are fetched in the same round as the slot
+        // columns, not after them
         const bool in = (int)lane < n0;
         const size_t i = base + lane;
-        const int32_t row = in ? S.obsrow[i] : -1;
+        const int32_t row_any = lane < cap ? __builtin_nontemporal_load(S.obsrow + i) : -1;
+        const int32_t row = in ? row_any : -1;
         const float x = in ? S.x[i] : 0.0f, y = in ? S.y[i] : 0.0f;
         const float rw = in ? S.rw[i] : 0.0f, rz = in ? S.rz[i] : 0.0f;
         const int32_t sp = in ? S.species[i] : 0, hp = in ? S.health[i] : 0;
@@ -1445,9 +1464,11 @@ hipError_t launch_tile_sum(const SimState &S, int parity, hipStream_t st)
 hipError_t launch_world_step(const SimState &S, const ObsTable &cur, int parity, hipStream_t st)
 {
     if (S.cap <= 128)
-        hipLaunchKernelGGL(world_step_kernel<128>, dim3(world_blocks(S.W)), dim3(256), 0, st, S, cur, parity);
+        hipLaunchKernelGGL(world_step_kernel<128>, dim3((S.W + kK1Worlds - 1) / kK1Worlds), dim3(64 * kK1Worlds), 0,
+                           st, S, cur, parity);
     else
-        hipLaunchKernelGGL(world_step_kernel<256>, dim3(world_blocks(S.W)), dim3(256), 0, st, S, cur, parity);
+        hipLaunchKernelGGL(world_step_kernel<256>, dim3((S.W + kK1Worlds - 1) / kK1Worlds), dim3(64 * kK1Worlds), 0,
+                           st, S, cur, parity);
     return hipGetLastError();
 }
 hipError_t launch_scan(const SimState &S, int parity, hipStream_t st, hipEvent_t done, bool plain_events)
