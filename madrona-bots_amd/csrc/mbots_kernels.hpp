@@ -32,7 +32,7 @@ struct SimState {
     uint32_t *overflow;             // [W] dropped births/respawns
     uint32_t *totals;               // [0] = N, [1..4] = per-species rows
     uint32_t *totals_host;          // mapped pinned mirror of totals (written by K2)
-    int32_t *tiles;                 // [2][ntiles][5] per-tile species/agent counts (K1 -> K2)
+    int32_t *tiles;                 // [2][ntiles][kTileBuckets][5] per-tile species/agent counts (K1 -> K2)
     unsigned long long *agent_steps;
     // K1's output half of the double-buffered columns the sensor reads (the
     // sensor of step t runs beside step t+1's K1; swap_state after each K1)
@@ -62,6 +62,9 @@ struct ObsTable {
 };
 
 uint32_t scan_tiles(uint32_t W);
+// K1 blocks add their counts into one of kTileBuckets copies of their tile's
+// counters (block index mod 8): fewer same-address atomics at K1's end
+constexpr int kTileBuckets = 8;
 hipError_t launch_init(const SimState &S, hipStream_t st);
 hipError_t launch_tile_sum(const SimState &S, int parity, hipStream_t st);
 hipError_t launch_world_step(const SimState &S, const ObsTable &cur, int parity, hipStream_t st);

@@ -188,7 +188,7 @@ size_t layout(mbots_handle *h, Arena &a)
     S.overflow = a.take<uint32_t>(W);
     S.totals = a.take<uint32_t>(8);
     S.ntiles = scan_tiles((uint32_t)W);
-    S.tiles = a.take<int32_t>((size_t)2 * S.ntiles * 5);
+    S.tiles = a.take<int32_t>((size_t)2 * S.ntiles * kTileBuckets * 5);
     S.agent_steps = a.take<unsigned long long>(1);
     S.x_out = a.take<float>(rows);
     S.y_out = a.take<float>(rows);
@@ -954,7 +954,7 @@ int mbots_load_checkpoint(mbots_handle *h, const void *src, uint64_t bytes)
         if (s.bytes) HIP_TRY(hipMemcpy(s.p, p, s.bytes, hipMemcpyHostToDevice));
         p += s.bytes;
     }
-    HIP_TRY(hipMemset(h->S.tiles, 0, (size_t)2 * h->S.ntiles * 5 * sizeof(int32_t)));
+    HIP_TRY(hipMemset(h->S.tiles, 0, (size_t)2 * h->S.ntiles * mbots::kTileBuckets * 5 * sizeof(int32_t)));
     h->tb = 0;
     h->parity = 0;
     h->last_join = -1;

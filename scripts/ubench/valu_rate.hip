@@ -1,0 +1,54 @@
+// VALU issue-rate microbenchmark (gfx950): wave64 VALU instructions per
+// SIMD-cycle for independent fp32 FMA / add chains and a compare+select mix,
+// at 8 waves per SIMD.  Prints instructions/s and cycles per instruction per
+// SIMD at the measured clock-free rate (assumes 2.4 GHz for the cycle figure).
+#include <hip/hip_runtime.h>
+#include <cstdio>
+
+template <int kMode>
+__global__ __launch_bounds__(256) void valu_kernel(float *out, int iters, float a, float b)
+{
+    float x0 = threadIdx.x * 1e-3f, x1 = x0 + 1, x2 = x0 + 2, x3 = x0 + 3, x4 = x0 + 4, x5 = x0 + 5,
+          x6 = x0 + 6, x7 = x0 + 7;
+    for (int i = 0; i < iters; ++i) {
+        if constexpr (kMode == 0) {   // 8 independent FMAs
+            x0 = __builtin_fmaf(x0, a, b); x1 = __builtin_fmaf(x1, a, b); x2 = __builtin_fmaf(x2, a, b);
+            x3 = __builtin_fmaf(x3, a, b); x4 = __builtin_fmaf(x4, a, b); x5 = __builtin_fmaf(x5, a, b);
+            x6 = __builtin_fmaf(x6, a, b); x7 = __builtin_fmaf(x7, a, b);
+        } else if constexpr (kMode == 1) {   // 8 independent adds
+            x0 += a; x1 += b; x2 += a; x3 += b; x4 += a; x5 += b; x6 += a; x7 += b;
+        } else {   // compare + select pairs (VOPC to vcc / SGPR + v_cndmask)
+            x0 = x0 < a ? x0 + b : x0 - b; x1 = x1 < a ? x1 + b : x1 - b;
+            x2 = x2 < a ? x2 + b : x2 - b; x3 = x3 < a ? x3 + b : x3 - b;
+        }
+    }
+    out[blockIdx.x * blockDim.x + threadIdx.x] = x0 + x1 + x2 + x3 + x4 + x5 + x6 + x7;
+}
+
+template <int kMode>
+void run(const char *name, int instr_per_iter, float *out)
+{
+    const int blocks = 256 * 8, iters = 4096;   // 8 blocks of 4 waves per CU = 8 waves / SIMD
+    hipEvent_t e0, e1;
+    hipEventCreate(&e0); hipEventCreate(&e1);
+    hipLaunchKernelGGL(valu_kernel<kMode>, dim3(blocks), dim3(256), 0, 0, out, iters, 0.999f, 0.001f);
+    hipEventRecord(e0);
+    hipLaunchKernelGGL(valu_kernel<kMode>, dim3(blocks), dim3(256), 0, 0, out, iters, 0.999f, 0.001f);
+    hipEventRecord(e1);
+    hipEventSynchronize(e1);
+    float ms = 0; hipEventElapsedTime(&ms, e0, e1);
+    const double instr = (double)blocks * 4 * iters * instr_per_iter;   // wave-instructions
+    const double rate = instr / (ms * 1e-3);
+    printf("{\"mode\": \"%s\", \"ms\": %.4f, \"wave_instr_per_s\": %.4g, \"cycles_per_instr_per_simd_at_2.4GHz\": %.3f}\n",
+           name, ms, rate, 1024 * 2.4e9 / rate);
+}
+
+int main()
+{
+    float *out; hipMalloc(&out, 256 * 8 * 256 * 4);
+    run<0>("fma x8", 8, out);
+    run<1>("add x8", 8, out);
+    run<2>("cmp+cndmask+add x4", 12, out);   // per pair: v_cmp, v_add, v_sub, v_cndmask ~ 3 VALU
+    hipFree(out);
+    return 0;
+}
