@@ -107,6 +107,19 @@ def load_kernel_stats():
     return out, os.path.relpath(files[-1], ROOT)
 
 
+def measured_valu_peak():
+    """The VALU issue rate measured on MI355X by scripts/ubench/valu_rate.hip
+    (profiles/*_valu_rate.json, the latest), or None."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_valu_rate.json")))
+    if not files:
+        return None
+    try:
+        return os.path.relpath(files[-1], ROOT), json.load(open(files[-1]))["measured_peak_wave_instr_per_s"]
+    except (OSError, ValueError, KeyError):
+        return None
+
+
 def load_profile(suffix, worlds):
     """profiles/*_<suffix>.json recorded at `worlds` (the latest), or None."""
     import glob
@@ -439,7 +452,13 @@ def main():
                     "launch_ms": per["sensor"], "achieved": rate, "peak": VALU_PEAK_INSTR_S,
                     "unit": "wave64 VALU instr/s", "frac": rate / VALU_PEAK_INSTR_S,
                     "source": vp[0],
-                    "note": "launch_ms is the sensor's event span inside the overlapped schedule"}
+                    "note": "launch_ms is the sensor's event span inside the overlapped schedule; "
+                            "peak: the guide's nominal 2 cycles per wave64 instruction"}
+                mp = measured_valu_peak()
+                if mp:
+                    out["sensor_valu"]["peak_measured"] = mp[1]
+                    out["sensor_valu"]["frac_measured"] = rate / mp[1]
+                    out["sensor_valu"]["peak_measured_source"] = mp[0]
         if args.gather:
             out["config5"] = {"what": "step + fused construct_obs + RCCL gather of obs [N,69] f32 "
                                       "and reward rows to rank 0 (harness/gather.py) + shift",

@@ -17,6 +17,13 @@ __global__ __launch_bounds__(256) void valu_kernel(float *out, int iters, float 
             x6 = __builtin_fmaf(x6, a, b); x7 = __builtin_fmaf(x7, a, b);
         } else if constexpr (kMode == 1) {   // 8 independent adds
             x0 += a; x1 += b; x2 += a; x3 += b; x4 += a; x5 += b; x6 += a; x7 += b;
+        } else if constexpr (kMode == 3) {   // 4 independent packed FMAs (2 fp32 lanes each)
+            typedef float f2 __attribute__((ext_vector_type(2)));
+            f2 p0 = {x0, x1}, p1 = {x2, x3}, p2 = {x4, x5}, p3 = {x6, x7};
+            const f2 va = {a, a}, vb = {b, b};
+            p0 = __builtin_elementwise_fma(p0, va, vb); p1 = __builtin_elementwise_fma(p1, va, vb);
+            p2 = __builtin_elementwise_fma(p2, va, vb); p3 = __builtin_elementwise_fma(p3, va, vb);
+            x0 = p0.x; x1 = p0.y; x2 = p1.x; x3 = p1.y; x4 = p2.x; x5 = p2.y; x6 = p3.x; x7 = p3.y;
         } else {   // compare + select pairs (VOPC to vcc / SGPR + v_cndmask)
             x0 = x0 < a ? x0 + b : x0 - b; x1 = x1 < a ? x1 + b : x1 - b;
             x2 = x2 < a ? x2 + b : x2 - b; x3 = x3 < a ? x3 + b : x3 - b;
@@ -48,7 +55,8 @@ int main()
     float *out; hipMalloc(&out, 256 * 8 * 256 * 4);
     run<0>("fma x8", 8, out);
     run<1>("add x8", 8, out);
-    run<2>("cmp+cndmask+add x4", 12, out);   // per pair: v_cmp, v_add, v_sub, v_cndmask ~ 3 VALU
+    run<2>("cmp+cndmask+add x4", 12, out);
+    run<3>("pk_fma x4 (8 fp32 FMAs)", 4, out);   // per pair: v_cmp, v_add, v_sub, v_cndmask ~ 3 VALU
     hipFree(out);
     return 0;
 }
