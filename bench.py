@@ -454,11 +454,14 @@ def main():
                     "source": vp[0],
                     "note": "launch_ms is the sensor's event span inside the overlapped schedule; "
                             "peak: the guide's nominal 2 cycles per wave64 instruction"}
+                # issue cost per wave64 VALU instruction per SIMD at 2.4 GHz: the
+                # nominal peak is 2 cycles; the microbenchmark's independent fp32
+                # FMA / add streams take ~4.9, its compare/select mix ~3.5
+                out["sensor_valu"]["cycles_per_instr_per_simd"] = 1024 * 2.4e9 / rate
                 mp = measured_valu_peak()
                 if mp:
-                    out["sensor_valu"]["peak_measured"] = mp[1]
-                    out["sensor_valu"]["frac_measured"] = rate / mp[1]
-                    out["sensor_valu"]["peak_measured_source"] = mp[0]
+                    out["sensor_valu"]["microbench_rate"] = mp[1]
+                    out["sensor_valu"]["microbench_source"] = mp[0]
         if args.gather:
             out["config5"] = {"what": "step + fused construct_obs + RCCL gather of obs [N,69] f32 "
                                       "and reward rows to rank 0 (harness/gather.py) + shift",

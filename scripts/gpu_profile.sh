@@ -22,6 +22,7 @@ mkdir -p gpurun_out/traffic_$TAG
 i=0; for c in FETCH_SIZE WRITE_SIZE; do i=$((i+1)); rm -rf gpurun_out/traffic_${TAG}_p$i; cp -r gpurun_out/pmc_${TAG}_$c gpurun_out/traffic_${TAG}_p$i; done
 python scripts/traffic.py gpurun_out/traffic_$TAG 65536 gpurun_out/${TAG}_traffic.json
 cp gpurun_out/prof_$TAG/run_kernel_stats.csv gpurun_out/${TAG}_kernel_stats.csv
+python scripts/timeline.py gpurun_out/prof_$TAG/run_kernel_trace.csv 100 > gpurun_out/${TAG}_timeline.txt
 grep '^{' gpurun_out/prof_$TAG.log | tail -1 > gpurun_out/${TAG}_bench_under_rocprof.json
 echo done
-# (run locally afterwards: cp gpurun_out/${TAG}_{traffic.json,valu.json,kernel_stats.csv,bench_under_rocprof.json} profiles/)
+# (run locally afterwards: cp gpurun_out/${TAG}_{traffic.json,valu.json,kernel_stats.csv,bench_under_rocprof.json,timeline.txt} profiles/)

@@ -1,4 +1,5 @@
 cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
-SEL="tests/test_parity_gpu.py tests/test_parity_large.py tests/test_checkpoint.py" ROUNDS=3 bash scripts/gpu_iter.sh || exit 1
-bash scripts/ab.sh 2 --worlds 4096 --steps 200 || exit 1
+timeout -k 10 600 python -u bench.py --steps 50 --warmup 20 --cpu-seconds 8 > gpurun_out/bench_full.log 2>&1 || { tail -20 gpurun_out/bench_full.log; exit 1; }
+tail -1 gpurun_out/bench_full.log
+TAG=r02 bash scripts/gpu_profile.sh
