@@ -440,22 +440,6 @@ int mbots_create(const mbots_config *cfg_in, mbots_handle **out)
     check(hipEventCreate(&h->ev_totals), "hipEventCreate");
     check(hipEventCreate(&h->ev_join[0]), "hipEventCreate");
     check(hipEventCreate(&h->ev_join[1]), "hipEventCreate");
-#ifdef MB_KNOBS
-    // occupancy experiment: the sensor stream on a CU subset spread evenly
-    if (const char *e = getenv("MBOTS_SENSOR_CUS")) {
-        hipDeviceProp_t prop;
-        check(hipGetDeviceProperties(&prop, cfg.gpu_id), "hipGetDeviceProperties");
-        const int ncu = prop.multiProcessorCount, k = atoi(e);
-        std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
-        for (int i = 0; i < ncu; ++i)
-            if ((i + 1) * k / ncu > i * k / ncu) mask[i / 32] |= 1u << (i % 32);
-        check(hipExtStreamCreateWithCUMask(&h->aux, (uint32_t)mask.size(), mask.data()),
-              "hipExtStreamCreateWithCUMask");
-    } else if (const char *e = getenv("MBOTS_AUX_PRIORITY")) {
-        check(hipStreamCreateWithPriority(&h->aux, hipStreamNonBlocking, atoi(e)),
-              "hipStreamCreateWithPriority");
-    } else
-#endif
     {
         // the sensor is the step's longer chain once the deferred Prev moves
         // left the caller's stream lighter: its stream gets the higher priority
