@@ -864,15 +864,13 @@ struct SensorLDS {
 };
 
 // pinhole offsets u = (2k + 1) / 24 - 1 forward, (2k' + 1) / 8 - 1 backward,
-// as the oracle's one rounding (2k - 23) (1/24) / exact (2k' - 7) / 8
-constexpr float u_of(int k)
+// as the oracle's one rounding (2k - 23) (1/24) / exact (2k' - 7) / 8;
+// computed in registers (a table in constant memory cost every wave a memory
+// round trip before its first load)
+__host__ __device__ constexpr float u_of(int k)
 {
     return k < 24 ? (float)(2 * k - 23) * (1.0f / 24.0f) : (float)(2 * (k - 24) - 7) * 0.125f;
 }
-#define MB_U4(k) u_of(k), u_of(k + 1), u_of(k + 2), u_of(k + 3)
-__constant__ float kURay[kSensor] = {MB_U4(0),  MB_U4(4),  MB_U4(8),  MB_U4(12),
-                                     MB_U4(16), MB_U4(20), MB_U4(24), MB_U4(28)};
-#undef MB_U4
 
 // (f, l) of object j in agent i's frame; order of the object
 template <class LDS>
@@ -1018,7 +1016,8 @@ __device__ __forceinline__ void run_survivors(LDS &L, int nf, int a0, int q0, in
 // the world's staged inputs, loaded as one batch of independent loads
 struct SensorPrefetch {
     uint64_t food;             // lane < 48: packed chunk record
-    uint32_t rot0;             // lane < 48: the chunk's package-0 rotation
+    uint32_t rot[kMaxPkg];     // lane < 48: the chunk's package rotations (all five: no
+                               // second round trip after the record's live mask)
     float x, y, rw, rz;        // lane < min(n, 64): agent slot `lane`
     int32_t sp;
     int n;
@@ -1031,7 +1030,9 @@ __device__ __forceinline__ void sensor_prefetch(const SimState &S, uint32_t w, u
     p.n = uniform(S.n[w]);
     p.rb = reinterpret_cast<const int4 *>(S.row_base)[w];
     p.food = lane < kNumChunks ? S.food[(size_t)w * kNumChunks + lane] : 0ull;
-    p.rot0 = lane < kNumChunks ? S.food_rot[(size_t)w * kNumPkg + lane] : 0u;
+#pragma unroll
+    for (int k = 0; k < kMaxPkg; ++k)
+        p.rot[k] = lane < kNumChunks ? S.food_rot[(size_t)w * kNumPkg + k * kNumChunks + lane] : 0u;
     // slots [0, min(cap, 64)), loaded without waiting for n (rows past n are
     // stale and never used)
     if (lane < S.cap) {
@@ -1079,7 +1080,7 @@ __global__ __launch_bounds__(64 * kSensorWorlds, kCap <= 128 ? MB_SENSOR_BLOCKS 
     if (w >= S.W) return;
     SensorLDS<kCap> &L = lds[wv];
     constexpr bool depth = kDepth;
-    if (lane < kSensor) L.u[lane] = kURay[lane];
+    if (lane < kSensor) L.u[lane] = u_of((int)lane);
     SensorPrefetch pf;
     sensor_prefetch(S, w, lane, pf);
     {
@@ -1088,7 +1089,7 @@ __global__ __launch_bounds__(64 * kSensorWorlds, kCap <= 128 ? MB_SENSOR_BLOCKS 
     const int n = cur.n;
 
     // ---- live food packages in (chunk, package) order -> objects [0, nf) ----
-    const int nf = stage_food(cur.food, cur.rot0, S.food_rot + (size_t)w * kNumPkg, lane, L.obj, L.frot);
+    const int nf = stage_food(cur.food, cur.rot, lane, L.obj, L.frot);
     // ---- agents -> objects [nf, nf + n) ----
     if ((int)lane < n) {
         float hx, hy;

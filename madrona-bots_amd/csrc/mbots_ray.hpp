@@ -174,13 +174,12 @@ MB_HD float box_z(const FoodBox &b, bool fwd)
 
 // live food packages of a world in (chunk, package) order -> objects [0, nf):
 // position and the box's (cos, sin).  Lane c (< 48) holds chunk c's packed
-// record and package 0's rotation (rot0, prefetched; the others are loaded
-// here from rot_w = food_rot + w * 5 * 48).  Each lane places its chunk's
+// record and its packages' rotations (prefetched).  Each lane places its chunk's
 // packages with their rotation word; then lane s < nf turns object s's word
 // into (cos, sin) -- one polynomial per lane instead of one per package of a
 // chunk.  Returns nf (== currentNumFood <= 30).
-__device__ __forceinline__ int stage_food(uint64_t rec, uint32_t rot0, const uint32_t *rot_w,
-                                          uint32_t lane, float2 *obj, float2 *frot)
+__device__ __forceinline__ int stage_food(uint64_t rec, const uint32_t (&rot)[kMaxPkg], uint32_t lane,
+                                          float2 *obj, float2 *frot)
 {
     const uint32_t live = (uint32_t)(rec >> 40) & 31u;
     const int cnt = __popc(live);
@@ -200,7 +199,7 @@ __device__ __forceinline__ int stage_food(uint64_t rec, uint32_t rot0, const uin
             const uint32_t xy = (uint32_t)(rec >> (8 * k)) & 0xFFu;
             if (s < kMaxFood) {   // live packages == currentNumFood <= 30
                 obj[s] = make_float2((float)(xy & 15u) + bx, (float)(xy >> 4) + by);
-                frot[s].x = __uint_as_float(k == 0 ? rot0 : rot_w[k * kNumChunks + lane]);
+                frot[s].x = __uint_as_float(rot[k]);
             }
             ++s;
         }
