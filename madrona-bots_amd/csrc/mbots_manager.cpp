@@ -436,10 +436,13 @@ int mbots_create(const mbots_config *cfg_in, mbots_handle **out)
     if (rc == MBOTS_OK)
         check(hipHostGetDevicePointer((void **)&S.totals_host, h->h_totals, 0),
               "hipHostGetDevicePointer");
-    // (default flags: these ride on kernel dispatches as their stop events)
-    check(hipEventCreate(&h->ev_totals), "hipEventCreate");
-    check(hipEventCreate(&h->ev_join[0]), "hipEventCreate");
-    check(hipEventCreate(&h->ev_join[1]), "hipEventCreate");
+    // (these ride on kernel dispatches as their stop events; synchronisation
+    // only: no timestamps, and a device-scope release -- the host reads only the
+    // pinned row counts, which K2 writes system-coherent and fences itself)
+    constexpr unsigned kSyncEvent = hipEventDisableTiming | hipEventReleaseToDevice;
+    check(hipEventCreateWithFlags(&h->ev_totals, kSyncEvent), "hipEventCreateWithFlags");
+    check(hipEventCreateWithFlags(&h->ev_join[0], kSyncEvent), "hipEventCreateWithFlags");
+    check(hipEventCreateWithFlags(&h->ev_join[1], kSyncEvent), "hipEventCreateWithFlags");
     {
         // the sensor is the step's longer chain once the deferred Prev moves
         // left the caller's stream lighter: its stream gets the higher priority
