@@ -24,6 +24,9 @@ namespace mbots {
 constexpr int kWorldsPerBlock = 4;
 constexpr int kTileWorlds = 1024;             // worlds per scan tile (K2 block)
 
+#ifndef MB_SHIFT_UNROLL
+#define MB_SHIFT_UNROLL 1   // items per thread per pass of the fused shift
+#endif
 #ifndef MB_NT
 #define MB_NT 35  // non-temporal stores: 1 K4, 2 K5, 4 K3a, 8 sensor output;
                   // non-temporal loads: 32 K4 sources, 64 K5 sources
@@ -801,12 +804,52 @@ __global__ __launch_bounds__(256) void move_kernel(const uint32_t *totals, const
     move_rows(totals, src_of, args);
 }
 
+// one segment of the fused shift, kU items per thread per pass: the kU
+// src_of loads, then the kU gathered loads, then the stores (each instruction
+// still coalesced over the wave: items idx + k * stride)
+template <typename T, int kIpr>
+__device__ __forceinline__ void gather_seg(const MoveSeg &sg, uint32_t N, const int32_t *src_of)
+{
+    constexpr int kU = MB_SHIFT_UNROLL;
+    const uint32_t items = N * kIpr;
+    const uint32_t stride = gridDim.x * blockDim.x;
+    const bool ntl = (MB_NT & 32) != 0, nts = (MB_NT & 1) != 0;
+    for (uint32_t i0 = blockIdx.x * blockDim.x + threadIdx.x; i0 < items; i0 += kU * stride) {
+        int32_t o[kU];
+#pragma unroll
+        for (int k = 0; k < kU; ++k) {
+            const uint32_t idx = i0 + k * stride;
+            o[k] = idx < items ? src_of[idx / kIpr] : -2;
+        }
+        T v[kU];
+#pragma unroll
+        for (int k = 0; k < kU; ++k) {
+            const uint32_t idx = i0 + k * stride;
+            v[k] = T{};
+            if (o[k] >= 0) v[k] = ld_stream(reinterpret_cast<const T *>(sg.src) + (size_t)o[k] * kIpr + idx % kIpr, ntl);
+        }
+#pragma unroll
+        for (int k = 0; k < kU; ++k) {
+            const uint32_t idx = i0 + k * stride;
+            if (o[k] != -2) {
+                st_stream(reinterpret_cast<T *>(sg.dst) + idx, v[k], nts);
+                if (sg.dst2) st_stream(reinterpret_cast<T *>(sg.dst2) + idx, v[k], nts);
+            }
+        }
+    }
+}
+
 // the fused shift (DESIGN.md "Deferred Prev moves"): Action / HiddenState
 // gathered from the other half into both the current and the Prev column
 __global__ __launch_bounds__(256) void shift_move_kernel(const uint32_t *totals, const int32_t *src_of,
                                                          MoveArgs args)
 {
-    move_rows(totals, src_of, args);
+    const MoveSeg &sg = args.seg[blockIdx.y];
+    const uint32_t N = totals[0];
+    if (sg.width == 8 && sg.ipr == 3) gather_seg<uint2, 3>(sg, N, src_of);
+    else if (sg.width == 16 && sg.ipr == 4) gather_seg<uint4, 4>(sg, N, src_of);
+    else if (sg.width == 16 && sg.ipr == 2) gather_seg<uint4, 2>(sg, N, src_of);
+    else move_rows(totals, src_of, args);
 }
 
 // ---------------------------------------------------------------------------
