@@ -1253,19 +1253,23 @@ __global__ __launch_bounds__(64 * kSensorWorlds, kCap <= 128 ? MB_SENSOR_BLOCKS 
                 for (int g = 1; g < kG; ++g)
                     if ((a0 >> 6) == g) r = __shfl(rows[g], i & 63);
             }
-            const float sgn = g < 6 ? 1.0f : -1.0f;
+            // backward pixels look along -(h + u r): the sign folded into the
+            // heading, sgn (h.x + u h.y) == (sgn h.x) + u (sgn h.y) exactly (IEEE
+            // rounding is sign-symmetric)
+            const float hxs = g < 6 ? h.x : -h.x, hys = g < 6 ? h.y : -h.y;
             const uint32_t kvs[4] = {kv4.x, kv4.y, kv4.z, kv4.w};
             const float us[4] = {u4.x, u4.y, u4.z, u4.w};
             uint32_t semv = 0, depv = 0;
 #pragma unroll
             for (int t = 0; t < 4; ++t) {
                 const float u = us[t];
-                const float dx = sgn * (h.x + u * h.y), dy = sgn * (h.y + u * (-h.x));
+                const float dx = hxs + u * hys, dy = hys + u * (-hxs);
                 const uint32_t kv = kvs[t];
                 const float oz = __uint_as_float(kv & ~kOrderMask);
                 const uint32_t order = kv & kOrderMask;
                 const bool obj = (kv != kNoKey) & beats_wall(p.x, p.y, dx, dy, oz);
-                const int spv = (int)L.sp[min((int)(order - kOrderAgent), n - 1) & (kCap - 1)];
+                // (any index in range: the species is used only for an agent's order)
+                const int spv = (int)L.sp[(order - kOrderAgent) & (kCap - 1)];
                 const int sem = obj ? (order < kOrderAgent ? 6 : spv) : 5;
                 semv |= (uint32_t)(uint8_t)(int8_t)sem << (8 * t);
                 if (depth) {
