@@ -183,8 +183,12 @@ __device__ void world_step(SimState &S, const ObsTable &cur, WorldLDS<kCap> &L, 
 #define MB_K1_WPB 8   // 4: K1 +2.5 %, and +7 % step at 4096 worlds; 16: +30 % K1
 #endif
 constexpr int kK1Worlds = MB_K1_WPB;          // worlds (waves) per K1 block
+// SGPRs capped at 80: the compiler's own choice (99, no spill at 80) admits only
+// 6 waves per SIMD (800 SGPRs per SIMD in 16-register granules plus 16), one
+// block in four fewer: K1 87 -> 78 us, step -1.7 %
 template <int kCap>
-__global__ __launch_bounds__(64 * kK1Worlds, (kCap <= 128 ? 32 : 16) / kK1Worlds) void world_step_kernel(
+__global__ __launch_bounds__(64 * kK1Worlds, (kCap <= 128 ? 32 : 16) / kK1Worlds)
+__attribute__((amdgpu_num_sgpr(80))) void world_step_kernel(
     SimState S, ObsTable cur, int parity)
 {
     __shared__ WorldLDS<kCap> lds[kK1Worlds];
