@@ -300,9 +300,12 @@ __device__ void world_step(SimState &S, const ObsTable &cur, WorldLDS<kCap> &L, 
     // ---- addFoodSystem (sim.cpp:363-387) + addFoodToChunk (:308-361) ----
     // The serial draw sequence uses at most 2 + 3 x 7 = 23 counters: lane k
     // computes draw ctr + k up front and the (wave-uniform) logic reads them
-    // with readlane.
+    // with readlane.  The draws past the ones addFood takes are the respawns'
+    // (speciesInfoSync below continues the same counter), so the 64 lanes'
+    // draws serve both phases: one Threefry per wave where there were three.
+    const uint32_t ctr0 = ctr;
+    const uint32_t dl = rng_draw(key, ctr + lane);
     {
-        const uint32_t dl = rng_draw(key, ctr + (lane & 31u));
         auto D = [&](uint32_t k) { return (uint32_t)__builtin_amdgcn_readlane((int)dl, (int)k); };
         uint32_t k = 0;
         if (sample_i32(D(k++), 0, 10) == 0) {
@@ -500,10 +503,20 @@ __device__ void world_step(SimState &S, const ObsTable &cur, WorldLDS<kCap> &L, 
     wave_sync();
     const int need0 = L.need[0], need1 = L.need[1], need2 = L.need[2], need3 = L.need[3];
     const int total_need = need0 + need1 + need2 + need3;
+    // respawn k's draws ctr + 2k, ctr + 2k + 1: from the lanes of dl while they
+    // lie within its 64 counters (all lanes shuffle, before the loop diverges)
+    const uint32_t ox = (ctr - ctr0) + 2u * lane;
+    const uint32_t dx0 = (uint32_t)__shfl((int)dl, (int)(ox & 63u));
+    const uint32_t dy0 = (uint32_t)__shfl((int)dl, (int)((ox + 1u) & 63u));
     for (int k = lane; k < total_need; k += 64) {
         int sp = k < need0 ? 1 : (k < need0 + need1 ? 2 : (k < need0 + need1 + need2 ? 3 : 4));
-        float x = u01(rng_draw(key, ctr + 2u * (uint32_t)k)) * kLx;
-        float y = u01(rng_draw(key, ctr + 2u * (uint32_t)k + 1u)) * kLy;
+        uint32_t bx = dx0, by = dy0;
+        if (k != (int)lane || ox + 1u >= 64u) {
+            bx = rng_draw(key, ctr + 2u * (uint32_t)k);
+            by = rng_draw(key, ctr + 2u * (uint32_t)k + 1u);
+        }
+        float x = u01(bx) * kLx;
+        float y = u01(by) * kLy;
         const int s = n1 + k;
         if (s < (int)cap) init_slot(L, s, x, y, sp, 100);
     }
