@@ -1047,7 +1047,7 @@ __device__ __forceinline__ void run_survivors(LDS &L, int nf, int a0, int q0, in
             if (food) {   // a far square: box_hit is the line test on its side
                 ha = box_line_hit(b, ua);
                 hb = box_line_hit(b, ub);
-                hf = fwd & box_line_hit(b, 0.0f);
+                hf = fwd & box_finder_hit(b);
                 kin = zkey(box_z(b, fwd), order);
             } else {
                 ha = far_pixel_hit(f, l, ua, fwd);
@@ -1225,9 +1225,10 @@ __global__ __launch_bounds__(64 * kSensorWorlds, kCap <= 128 ? MB_SENSOR_BLOCKS 
                     // the wedge's survivors go: step -3 %)
                     const float rf = __builtin_amdgcn_rcpf(f);
                     const float uc = l * rf;
-                    const float ar = (food ? 1.42f : 1.0f) * fabsf(rf);
+                    // (ar carries the 1.001 margin itself: every factor only grows)
+                    const float ar = (food ? 1.42f * 1.001f : 1.001f) * fabsf(rf);
                     const float w = ar * __builtin_fmaf(ar, fabsf(uc), __builtin_fmaf(0.5f * uc, uc, 1.0f)) *
-                                    __builtin_fmaf(1.2f * ar, ar, 1.0f) * 1.001f + 1e-4f;
+                                    __builtin_fmaf(1.2f * ar, ar, 1.0f) + 1e-4f;
                     const bool fwd = f > 0.0f;
                     const float sc = fwd ? 12.0f : 4.0f;
                     const float s = __builtin_fmaf(uc, sc, sc - 0.5f);

@@ -151,6 +151,13 @@ MB_HD bool box_line_hit(const FoodBox &b, float u)
     return fabsf(b.l - u * b.f) <= fabsf(b.q - u * b.p) + fabsf(b.p + u * b.q);
 }
 
+// box_line_hit at u = 0 (the finder ray): for finite operands x - 0 y and
+// x + 0 y are x up to the sign of a zero, which fabsf drops
+MB_HD bool box_finder_hit(const FoodBox &b)
+{
+    return fabsf(b.l) <= fabsf(b.q) + fabsf(b.p);
+}
+
 MB_HD float slab_lo(float m, float b)
 {
     return b > 0.0f ? (m - 1.0f) / b : b < 0.0f ? (m + 1.0f) / b : -__builtin_inff();
