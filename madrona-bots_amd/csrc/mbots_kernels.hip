@@ -196,13 +196,16 @@ __attribute__((amdgpu_num_sgpr(80))) void world_step_kernel(
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t w = uniform(blockIdx.x * kK1Worlds + wv);
     if (w < S.W) world_step(S, cur, lds[wv], w, lane);
-    int32_t *tiles = S.tiles + (size_t)parity * S.ntiles * kTileBuckets * 5;
+    // counter-major tile buckets: [counter][tile][bucket] (K2 reads one
+    // counter's buckets as contiguous 16-B words)
+    const size_t nent = (size_t)S.ntiles * kTileBuckets;
+    int32_t *tiles = S.tiles + (size_t)parity * 5 * nent;
     if constexpr (kK1Worlds == 1) {
         // one world per block: its species/agent counts go straight to the K2
         // scan tile (no block barrier: a block's LDS frees as its world ends)
         if (w < S.Wx && lane < 5) {   // (a shard ghost, w >= Wx, is not counted)
             const int32_t *sc = lds[0].scount;
-            atomicAdd(&tiles[((w / kTileWorlds) * kTileBuckets + blockIdx.x % kTileBuckets) * 5 + lane],
+            atomicAdd(&tiles[lane * nent + (w / kTileWorlds) * kTileBuckets + blockIdx.x % kTileBuckets],
                       lane < 4 ? sc[lane] : sc[0] + sc[1] + sc[2] + sc[3]);
         }
     } else {
@@ -218,7 +221,7 @@ __attribute__((amdgpu_num_sgpr(80))) void world_step_kernel(
 #pragma unroll
             for (int k = 0; k < kK1Worlds; ++k) v += blk[k][threadIdx.x];
             const uint32_t tile = (blockIdx.x * kK1Worlds) / kTileWorlds;
-            atomicAdd(&tiles[(tile * kTileBuckets + blockIdx.x % kTileBuckets) * 5 + threadIdx.x], v);
+            atomicAdd(&tiles[threadIdx.x * nent + tile * kTileBuckets + blockIdx.x % kTileBuckets], v);
         }
     }
 }
@@ -586,13 +589,18 @@ __global__ __launch_bounds__(1024) void scan_kernel(SimState S, int parity)
     __shared__ int32_t s_wave[16][5];
     const int t = threadIdx.x, b = blockIdx.x;
     const int wv = t >> 6, lane = t & 63;
-    const int32_t *tiles = S.tiles + (size_t)parity * S.ntiles * kTileBuckets * 5;
-    // wave k < 5 sums counter k over the tiles' buckets, 64 per pass
+    const uint32_t nent = S.ntiles * kTileBuckets;   // a multiple of 8: 16-B words
+    const int32_t *tiles = S.tiles + (size_t)parity * 5 * nent;
+    // wave k < 5 sums counter k over the tiles' buckets, four contiguous
+    // buckets (of one tile) per 16-B load, 256 per pass
     if (wv < 5) {
         int32_t pre = 0, tot = 0;
-        for (uint32_t tt = lane; tt < S.ntiles * kTileBuckets; tt += 64) {
-            const int32_t v = tiles[tt * 5 + wv];
-            if ((int)(tt / kTileBuckets) < b) pre += v;
+        const int4 *tk = reinterpret_cast<const int4 *>(tiles + (size_t)wv * nent);
+#pragma unroll 4
+        for (uint32_t q = lane; q < nent / 4; q += 64) {
+            const int4 v4 = tk[q];
+            const int32_t v = v4.x + v4.y + v4.z + v4.w;
+            if ((int)(q / (kTileBuckets / 4)) < b) pre += v;
             tot += v;
         }
         pre = wave_incl_scan(pre);
@@ -639,7 +647,9 @@ __global__ __launch_bounds__(1024) void scan_kernel(SimState S, int parity)
         reinterpret_cast<int4 *>(S.row_base)[w] = rb;
         S.world_off[w] = off;
     }
-    if (t < 5 * kTileBuckets) S.tiles[((size_t)(parity ^ 1) * S.ntiles + b) * kTileBuckets * 5 + t] = 0;
+    if (t < 5 * kTileBuckets)   // this tile's buckets of the other parity, for the next step
+        S.tiles[(size_t)(parity ^ 1) * 5 * nent + (size_t)(t / kTileBuckets) * nent + (size_t)b * kTileBuckets +
+                t % kTileBuckets] = 0;
     if (b == 0 && t == 0) {
         S.totals[0] = (uint32_t)s_tot[4];
         for (int k = 0; k < 4; ++k) S.totals[1 + k] = (uint32_t)s_tot[k];
@@ -677,11 +687,14 @@ __global__ __launch_bounds__(1024) void tile_sum_kernel(SimState S, int parity)
     }
     __syncthreads();
     if (t < 5 * kTileBuckets) {   // the tile's sum in bucket 0, the other buckets and parity cleared
+        const size_t nent = (size_t)S.ntiles * kTileBuckets;
+        const int k = t / kTileBuckets, bk = t % kTileBuckets;
         int32_t run = 0;
-        if (t < 5)
-            for (int i = 0; i < 16; ++i) run += s_wave[i][t];
-        S.tiles[((size_t)parity * S.ntiles + b) * kTileBuckets * 5 + t] = run;
-        S.tiles[((size_t)(parity ^ 1) * S.ntiles + b) * kTileBuckets * 5 + t] = 0;
+        if (bk == 0)
+            for (int i = 0; i < 16; ++i) run += s_wave[i][k];
+        const size_t e = (size_t)k * nent + (size_t)b * kTileBuckets + bk;
+        S.tiles[(size_t)parity * 5 * nent + e] = run;
+        S.tiles[(size_t)(parity ^ 1) * 5 * nent + e] = 0;
     }
 }
 

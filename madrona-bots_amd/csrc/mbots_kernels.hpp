@@ -32,7 +32,7 @@ struct SimState {
     uint32_t *overflow;             // [W] dropped births/respawns
     uint32_t *totals;               // [0] = N, [1..4] = per-species rows
     uint32_t *totals_host;          // mapped pinned mirror of totals (written by K2)
-    int32_t *tiles;                 // [2][ntiles][kTileBuckets][5] per-tile species/agent counts (K1 -> K2)
+    int32_t *tiles;                 // [2][5][ntiles][kTileBuckets] per-tile species/agent counts (K1 -> K2)
     unsigned long long *agent_steps;
     // K1's output half of the double-buffered columns the sensor reads (the
     // sensor of step t runs beside step t+1's K1; swap_state after each K1)
