@@ -777,11 +777,10 @@ __global__ __launch_bounds__(256) void export_rows_kernel(SimState S, ObsTable n
 // A step launches only the prev-sensor part; the other parts are deferred
 // (DESIGN.md "Deferred Prev moves") and run from the host's materialisation
 // points, or fused with the shift (shift_move_kernel: Action / HiddenState into
-// both the current and the Prev column).
+// the Prev columns, the current ones left as their views).
 // ---------------------------------------------------------------------------
 struct MoveSeg {
     void *dst;
-    void *dst2;       // a second destination (the fused shift's Prev column) or null
     const void *src;
     uint32_t width;   // bytes per item: 4, 8 or 16
     uint32_t ipr;     // items per row
@@ -800,7 +799,6 @@ __device__ __forceinline__ void move_item(const MoveSeg &sg, uint32_t idx, int32
     T v{};
     if (o >= 0) v = ld_stream(reinterpret_cast<const T *>(sg.src) + (size_t)o * sg.ipr + part, (MB_NT & 32) != 0);
     st_stream(reinterpret_cast<T *>(sg.dst) + idx, v, nt);
-    if (sg.dst2) st_stream(reinterpret_cast<T *>(sg.dst2) + idx, v, nt);
 }
 
 __device__ __forceinline__ void move_rows(const uint32_t *totals, const int32_t *src_of,
@@ -861,16 +859,14 @@ __device__ __forceinline__ void gather_seg(const MoveSeg &sg, uint32_t N, const 
 #pragma unroll
         for (int k = 0; k < kU; ++k) {
             const uint32_t idx = i0 + k * stride;
-            if (o[k] != -2) {
-                st_stream(reinterpret_cast<T *>(sg.dst) + idx, v[k], nts);
-                if (sg.dst2) st_stream(reinterpret_cast<T *>(sg.dst2) + idx, v[k], nts);
-            }
+            if (o[k] != -2) st_stream(reinterpret_cast<T *>(sg.dst) + idx, v[k], nts);
         }
     }
 }
 
 // the fused shift (DESIGN.md "Deferred Prev moves"): Action / HiddenState
-// gathered from the other half into both the current and the Prev column
+// gathered from the other half into the Prev columns (the current ones are
+// left as their views: DESIGN.md "Aliased current Action / HiddenState")
 __global__ __launch_bounds__(256) void shift_move_kernel(const uint32_t *totals, const int32_t *src_of,
                                                          MoveArgs args)
 {
@@ -1577,16 +1573,18 @@ hipError_t launch_move(const SimState &S, const ObsTable &cur, const ObsTable &n
 {
     MoveArgs m{};
     int k = 0;
-    auto add = [&](void *d, const void *s, uint32_t width, uint32_t ipr, uint32_t xform = 0,
-                   void *d2 = nullptr) {
-        m.seg[k++] = MoveSeg{d, d2, s, width, ipr, xform};
+    auto add = [&](void *d, const void *s, uint32_t width, uint32_t ipr, uint32_t xform = 0) {
+        m.seg[k++] = MoveSeg{d, s, width, ipr, xform};
     };
     // after a lazy shift the six Prev* columns it left are the current ones
     const bool lz = prev_lazy != 0;
-    if (parts & (kMoveAH | kMoveAHShift)) {
-        const bool sh = (parts & kMoveAHShift) != 0;
-        add(nxt.action, cur.action, 8, 3, 0, sh ? nxt.paction : nullptr);
-        add(nxt.hidden, cur.hidden, 16, 4, 0, sh ? nxt.phidden : nullptr);
+    if (parts & kMoveAH) {
+        add(nxt.action, cur.action, 8, 3);
+        add(nxt.hidden, cur.hidden, 16, 4);
+    } else if (parts & kMoveAHShift) {   // the fused shift: the Prev columns (the
+                                        // current ones become their views)
+        add(nxt.paction, cur.action, 8, 3);
+        add(nxt.phidden, cur.hidden, 16, 4);
     }
     if (parts & kMoveSensor) {
         add(nxt.psem, cur.sem, 16, 2);                   // prev sensor <- last step's sensor

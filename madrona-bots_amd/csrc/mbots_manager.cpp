@@ -88,6 +88,12 @@ struct mbots_handle {
     bool ah_pending[2] = {false, false};
     bool six_pending[2] = {false, false};
     bool six_lazy[2] = {false, false};
+    // the half's current Action / HiddenState column is its Prev column: a
+    // fused shift gathered the moved rows into PrevAction / PrevHiddenState only
+    // (the learner overwrites the current ones next); readers go through
+    // src_view, accessors copy first (materialize_cur_ah)
+    bool a_alias[2] = {false, false};
+    bool h_alias[2] = {false, false};
     bool prev_lazy[2] = {false, false};   // table half's six shift-owned Prev* columns are
                                           // still its current ones (lazy shift, K5)
     int forced = 0;                   // deferred parts the caller's reads needed since the
@@ -208,6 +214,16 @@ size_t layout(mbots_handle *h, Arena &a)
 
 hipStream_t as_stream(void *s) { return reinterpret_cast<hipStream_t>(s); }
 
+// table half `half` as its readers see it: an aliased current Action /
+// HiddenState column read from its Prev column
+mbots::ObsTable src_view(const mbots_handle *h, int half)
+{
+    mbots::ObsTable t = h->T[half];
+    if (h->a_alias[half]) t.action = t.paction;
+    if (h->h_alias[half]) t.hidden = t.phidden;
+    return t;
+}
+
 // make the caller's stream (the one step() ran on) wait for the sensor rows
 int wait_sensor(mbots_handle *h)
 {
@@ -254,16 +270,39 @@ int materialize_prev_ah(mbots_handle *h, hipStream_t st)
 }
 
 // the deferred Action / HiddenState move of the current half (K1, the learner
-// and every accessor of the two columns need it; a shift fuses it)
-int materialize_cur_ah(mbots_handle *h, hipStream_t st)
+// and every accessor of the two columns need it; a shift fuses it); then the
+// columns of `alias_cols` (1 Action, 2 HiddenState) a fused shift left as
+// views of their Prev columns are copied out
+int sync_totals(mbots_handle *h);
+int materialize_cur_ah(mbots_handle *h, hipStream_t st, int alias_cols = 3)
 {
-    if (!h->cur_ah_pending[h->tb]) return MBOTS_OK;
+    const int tb = h->tb;
+    if (h->cur_ah_pending[tb]) {
+        HIP_TRY(hipSetDevice(h->device));
+        const mbots::ObsTable src = src_view(h, tb ^ 1);
+        const int rc = timed(h, MBOTS_TK_MOVE, st, [&] {
+            return mbots::launch_move(h->S, src, h->T[tb], 0, mbots::kMoveAH, st);
+        });
+        if (rc) return rc;
+        h->cur_ah_pending[tb] = false;
+    }
+    const bool ca = (alias_cols & 1) && h->a_alias[tb], ch = (alias_cols & 2) && h->h_alias[tb];
+    if (!ca && !ch) return MBOTS_OK;
     HIP_TRY(hipSetDevice(h->device));
-    const int rc = timed(h, MBOTS_TK_MOVE, st, [&] {
-        return mbots::launch_move(h->S, h->T[h->tb ^ 1], h->T[h->tb], 0, mbots::kMoveAH, st);
+    int rc = sync_totals(h);
+    if (rc) return rc;
+    const size_t N = h->h_totals[0];
+    const mbots::ObsTable &t = h->T[tb];
+    rc = timed(h, MBOTS_TK_MOVE, st, [&] {
+        hipError_t e = hipSuccess;
+        if (ca && N) e = hipMemcpyAsync(t.action, t.paction, N * 6 * sizeof(int32_t), hipMemcpyDeviceToDevice, st);
+        if (e == hipSuccess && ch && N)
+            e = hipMemcpyAsync(t.hidden, t.phidden, N * mbots::kHidden * sizeof(float), hipMemcpyDeviceToDevice, st);
+        return e;
     });
     if (rc) return rc;
-    h->cur_ah_pending[h->tb] = false;
+    if (ca) h->a_alias[tb] = false;
+    if (ch) h->h_alias[tb] = false;
     return MBOTS_OK;
 }
 
@@ -505,7 +544,9 @@ int mbots_step(mbots_handle *h, void *stream)
     HIP_TRY(hipSetDevice(h->device));
     hipStream_t st = as_stream(stream);
     h->last_stream = st;
-    const mbots::ObsTable &cur = h->T[h->tb];
+    // K1 reads the learner's actions through the half's view (an aliased
+    // Action column is its PrevAction), and so do this step's moves
+    const mbots::ObsTable cur = src_view(h, h->tb);
     const mbots::ObsTable &nxt = h->T[h->tb ^ 1];
     int rc;
     const int par = h->parity;
@@ -524,7 +565,7 @@ int mbots_step(mbots_handle *h, void *stream)
     // no shift since the last step: its deferred Prev moves first
     if (h->six_pending[h->tb] && (rc = materialize_prev(h, st))) return rc;
     if ((rc = materialize_prev_ah(h, st))) return rc;
-    if ((rc = materialize_cur_ah(h, st))) return rc;
+    if ((rc = materialize_cur_ah(h, st, 0))) return rc;
     if ((rc = materialize_psem(h, st))) return rc;   // before this step's sensor rewrites its source
     // K1 reads the finder slots the previous step's sensor wrote, and writes the
     // state half that sensor read; the halves swap after K1.
@@ -582,6 +623,7 @@ int mbots_step(mbots_handle *h, void *stream)
     h->tb ^= 1;
     // the new half's Prev* columns: eight moves deferred (a shift overwrites them)
     h->prev_lazy[h->tb] = false;
+    h->a_alias[h->tb] = h->h_alias[h->tb] = false;
     h->cur_ah_pending[h->tb] = true;
 #ifndef MB_NO_FORK
     h->psem_pending[h->tb] = true;
@@ -606,28 +648,38 @@ int mbots_shift_observations(mbots_handle *h, void *stream)
     HIP_TRY(hipSetDevice(h->device));
     hipStream_t st = as_stream(stream);
     h->last_stream = st;
-    // Action / HiddenState now (the learner overwrites them next); the other six
-    // Prev* columns stay views of the current ones until the next step or an
-    // accessor needs them (K5, lazy shift)
-    // (Action / HiddenState still in the other half: one gather writes them and
-    // their Prev copies -- the fused shift)
-    // (and the prev sensor rides along when still pending)
-    const bool fused = h->cur_ah_pending[h->tb];
-    const bool with_psem = fused && h->psem_pending[h->tb];
-    const int rc = timed(h, MBOTS_TK_SHIFT, st, [&] {
-        return fused ? mbots::launch_move(h->S, h->T[h->tb ^ 1], h->T[h->tb], 0,
-                                          mbots::kMoveAHShift | (with_psem ? mbots::kMoveSensor : 0), st)
-                     : mbots::launch_shift(h->S, h->T[h->tb], mbots::kShiftEager, st);
-    });
+    // Action / HiddenState now; the other six Prev* columns stay views of the
+    // current ones until the next step or an accessor needs them (K5, lazy
+    // shift).  Action / HiddenState still in the other half: one gather writes
+    // their Prev copies, and the current columns become views of those (the
+    // learner overwrites them next; DESIGN.md "Aliased current Action /
+    // HiddenState") -- the fused shift; the prev sensor rides along when still
+    // pending.
+    const int tb = h->tb;
+    const bool fused = h->cur_ah_pending[tb];
+    const bool with_psem = fused && h->psem_pending[tb];
+    int rc = MBOTS_OK;
+    if (fused) {
+        const mbots::ObsTable src = src_view(h, tb ^ 1);
+        rc = timed(h, MBOTS_TK_SHIFT, st, [&] {
+            return mbots::launch_move(h->S, src, h->T[tb], 0,
+                                      mbots::kMoveAHShift | (with_psem ? mbots::kMoveSensor : 0), st);
+        });
+    } else if (!(h->a_alias[tb] && h->h_alias[tb])) {   // both aliased: already equal
+        if ((rc = materialize_cur_ah(h, st))) return rc;
+        rc = timed(h, MBOTS_TK_SHIFT, st,
+                   [&] { return mbots::launch_shift(h->S, h->T[tb], mbots::kShiftEager, st); });
+    }
     if (rc == MBOTS_OK) {
         // Action / HiddenState and every Prev* column but the sensor's are the
         // shift's now: a later read of them is not the step's deferred move
         h->prefetched &= mbots::kMoveSensor;
-        h->cur_ah_pending[h->tb] = false;
-        if (with_psem) h->psem_pending[h->tb] = false;
-        h->prev_lazy[h->tb] = true;
-        h->ah_pending[h->tb] = false;   // the shift wrote PrevAction / PrevHiddenState
-        h->six_pending[h->tb] = false;  // ... and made the six the current columns
+        if (fused) h->a_alias[tb] = h->h_alias[tb] = true;
+        h->cur_ah_pending[tb] = false;
+        if (with_psem) h->psem_pending[tb] = false;
+        h->prev_lazy[tb] = true;
+        h->ah_pending[tb] = false;   // the shift wrote PrevAction / PrevHiddenState
+        h->six_pending[tb] = false;  // ... and made the six the current columns
     }
     return rc;
 }
@@ -670,7 +722,7 @@ int mbots_export(mbots_handle *h, int32_t id, mbots_tensor *out)
         break;
     case MBOTS_EXPORT_ACTION: case MBOTS_EXPORT_HIDDEN_STATE:
         need = mbots::kMoveAH;
-        if ((rc = materialize_cur_ah(h, h->last_stream))) return rc;
+        if ((rc = materialize_cur_ah(h, h->last_stream, id == MBOTS_EXPORT_ACTION ? 1 : 2))) return rc;
         break;
     case MBOTS_EXPORT_PREV_SENSOR_SEMANTIC: case MBOTS_EXPORT_PREV_SENSOR_DEPTH:
         need = mbots::kMoveSensor;
@@ -744,7 +796,7 @@ int mbots_set_action(mbots_handle *h, uint32_t row, const int32_t action[6])
         return MBOTS_OK;
     }
     const int owed = pending_mask(h);
-    if ((rc = materialize_cur_ah(h, h->last_stream))) return rc;
+    if ((rc = materialize_cur_ah(h, h->last_stream, 1))) return rc;
     note_use(h, mbots::kMoveAH, owed);
     HIP_TRY(hipMemcpyAsync(h->T[h->tb].action + (size_t)row * 6, action, 6 * sizeof(int32_t),
                            hipMemcpyHostToDevice, h->last_stream));
@@ -780,12 +832,18 @@ int mbots_write_synthetic_actions(mbots_handle *h, uint32_t seed, uint32_t step,
     hipStream_t st = as_stream(stream);
     h->last_stream = st;
     const int owed = pending_mask(h);
-    int rc = materialize_cur_ah(h, st);
+    // the writer rewrites every live row's Action (and HiddenState with
+    // write_hidden): an aliased column of those is simply written, not copied
+    int rc = materialize_cur_ah(h, st, 0);
     if (rc) return rc;
     note_use(h, mbots::kMoveAH, owed);
-    return timed(h, MBOTS_TK_ACTIONS, st, [&] {
+    rc = timed(h, MBOTS_TK_ACTIONS, st, [&] {
         return mbots::launch_synthetic_actions(h->S, h->T[h->tb], seed, step, write_hidden, st);
     });
+    if (rc) return rc;
+    h->a_alias[h->tb] = false;
+    if (write_hidden) h->h_alias[h->tb] = false;
+    return MBOTS_OK;
 }
 
 int mbots_construct_obs(mbots_handle *h, int32_t prev, float *out, uint64_t out_rows, void *stream)
@@ -950,6 +1008,7 @@ int mbots_load_checkpoint(mbots_handle *h, const void *src, uint64_t bytes)
     h->six_pending[0] = h->six_pending[1] = false;
     h->cur_ah_pending[0] = h->cur_ah_pending[1] = false;
     h->psem_pending[0] = h->psem_pending[1] = false;
+    h->a_alias[0] = h->a_alias[1] = h->h_alias[0] = h->h_alias[1] = false;
     h->forced = 0;
     h->prefetched = 0;
     h->steps = 1;

@@ -1,5 +1,8 @@
-cd $GRAFT_REPO_ROOT
-export TMPDIR=/tmp
-timeout -k 10 600 python -u bench.py --steps 50 --warmup 20 --cpu-seconds 8 > gpurun_out/bench_full.log 2>&1 || { tail -20 gpurun_out/bench_full.log; exit 1; }
-tail -1 gpurun_out/bench_full.log
-TAG=r02 bash scripts/gpu_profile.sh
+#!/bin/bash
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+timeout -k 10 400 python -u -m pytest tests/test_parity_gpu.py tests/test_gpu_basic.py tests/test_checkpoint.py -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/pytest_q.log 2>&1
+rc=$?; tail -3 gpurun_out/pytest_q.log
+if [ $rc -ne 0 ]; then grep -E "^E |Error|assert" gpurun_out/pytest_q.log | head -20; exit $rc; fi
+scripts/ab_libs.sh 3 build_var/libmbots_base.so build_var/libmbots_alias.so
