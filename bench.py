@@ -332,6 +332,9 @@ def main():
             gather_s[0] += time.perf_counter() - g0
         mgr.shift_observations()
         if k in ev:
+            # the span ends when both chains have: the sensor's stream joined
+            # first (the next step's K1 waits for it anyway)
+            mgr.join()
             ev[k][1].record()
         mgr.write_synthetic_actions(ACTION_SEED, t + 1)
     torch.cuda.synchronize()
@@ -407,7 +410,8 @@ def main():
                 "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                 "algorithmic_bytes_per_launch": nb, "avg_launch_ms": span_ms,
                 "timing": f"HIP events on the launch stream around every {max(1, args.span_every)}"
-                          "th step()+shift() of the timed region"}
+                          "th step()+shift() of the timed region, the end event after "
+                          "joining the sensor's stream (both chains of the step)"}
         # the same span priced at the bytes this design must move in this loop
         nb_lazy = LAZY_BYTES_PER_AGENT * mean_agents + 1952.0 * W
         lazy_gbs = nb_lazy / (span_ms * 1e-3) / 1e9

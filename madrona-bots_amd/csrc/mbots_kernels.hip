@@ -715,6 +715,9 @@ __global__ __launch_bounds__(256) void export_rows_kernel(SimState S, ObsTable n
     if (w >= S.W) return;
     const size_t base = (size_t)w * S.cap;
     const int n = uniform(S.n[w]);
+    // slot `lane`'s species loaded beside the count (rows past n are stale
+    // and never used)
+    const int32_t sp0 = (int)lane < (int)S.cap ? S.species[base + lane] : 0;
     const int4 rb = reinterpret_cast<const int4 *>(S.row_base)[w];
     const float4 rew = reinterpret_cast<const float4 *>(S.sreward)[w];
     const bool fixed = (S.flags & kFlagRewardFixed) != 0;
@@ -724,7 +727,7 @@ __global__ __launch_bounds__(256) void export_rows_kernel(SimState S, ObsTable n
     for (int b = 0; b < n; b += 64) {
         const int i = b + (int)lane;
         const bool active = i < n;
-        const int32_t sp = active ? S.species[base + i] : 0;
+        const int32_t sp = active ? (b == 0 ? sp0 : S.species[base + i]) : 0;
         const uint64_t m1 = ballot64(sp == 1), m2 = ballot64(sp == 2);
         const uint64_t m3 = ballot64(sp == 3), m4 = ballot64(sp == 4);
         int32_t row = 0;
@@ -1491,9 +1494,13 @@ __global__ __launch_bounds__(256) void synthetic_actions_kernel(SimState S, ObsT
     const size_t base = (size_t)w * S.cap;
     const uint32_t gw = S.world_offset + w;
     const int n = uniform(S.n[w]);
+    // slot `lane`'s row loaded beside the count, and its draw computed while
+    // both loads are in flight (rows past n are stale and never used)
+    const int32_t r0 = (int)lane < (int)S.cap ? S.obsrow[base + lane] : 0;
+    const uint32_t k0 = threefry2x32(seed, step, gw, lane).x % 6u;
     for (int i = lane; i < n; i += 64) {
-        const size_t r = (size_t)S.obsrow[base + i];
-        const uint32_t k = threefry2x32(seed, step, gw, (uint32_t)i).x % 6u;
+        const size_t r = i < 64 ? (size_t)r0 : (size_t)S.obsrow[base + i];
+        const uint32_t k = i < 64 ? k0 : threefry2x32(seed, step, gw, (uint32_t)i).x % 6u;
         int2 *ap = reinterpret_cast<int2 *>(t.action + r * 6);
         ap[0] = make_int2(k == 0, k == 1);
         ap[1] = make_int2(k == 2, k == 3);

@@ -2,7 +2,7 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
-timeout -k 10 400 python -u -m pytest tests/test_parity_gpu.py tests/test_gpu_basic.py tests/test_checkpoint.py -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/pytest_q.log 2>&1
-rc=$?; tail -3 gpurun_out/pytest_q.log
+timeout -k 10 300 python -u -m pytest tests/test_parity_gpu.py -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/pytest_q.log 2>&1
+rc=$?; tail -2 gpurun_out/pytest_q.log
 if [ $rc -ne 0 ]; then grep -E "^E |Error|assert" gpurun_out/pytest_q.log | head -20; exit $rc; fi
-scripts/ab_libs.sh 3 build_var/libmbots_base.so build_var/libmbots_alias.so
+scripts/ab_libs.sh 3 build_var/libmbots_head.so build_var/libmbots_wr.so build_var/libmbots_wrk3.so -- --stream-priority -1
