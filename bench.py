@@ -186,6 +186,9 @@ def reference_loop(W, args, rank, world_size, dev, distributed, label):
         m.write_synthetic_actions(ACTION_SEED, t + 1, True)  # :136-137 actions + memory
         return ends, rew, hp, obs, prev, ph
 
+    # a small-world step is ~0.14 ms and host-latency-bound: time at least
+    # 400 steps so a host hiccup does not move the line (100 steps: +-40 %)
+    steps = args.steps if W > 8192 else max(args.steps, 400)
     m.write_synthetic_actions(ACTION_SEED, 0, True)
     for t in range(args.warmup):
         one(t)
@@ -195,7 +198,7 @@ def reference_loop(W, args, rank, world_size, dev, distributed, label):
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for t in range(args.warmup, args.warmup + args.steps):
+    for t in range(args.warmup, args.warmup + steps):
         one(t)
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
@@ -212,19 +215,19 @@ def reference_loop(W, args, rank, world_size, dev, distributed, label):
     ktimes = {}
     if not args.no_kernel_timing:
         m.enable_kernel_timing(True)
-        t = args.warmup + args.steps
-        for k in range(min(args.steps, 30)):
+        t = args.warmup + steps
+        for k in range(min(steps, 30)):
             one(t + k)
         torch.cuda.synchronize()
         ktimes = {k: round(ms / n, 5) for k, (ms, n) in m.kernel_times().items() if n}
         m.enable_kernel_timing(False)
     del m
-    n_mean = n_local / args.steps
-    ms = el / args.steps * 1e3
+    n_mean = n_local / steps
+    ms = el / steps * 1e3
     nb = algorithmic_bytes(n_mean, W) + LOOP_EXTRA_PER_AGENT * n_mean
     gbs = nb / (ms * 1e-3) / 1e9
     return {"worlds_per_gpu": W, "value": total / el, "unit": "agent-steps/s",
-            "ms_per_step": ms, "n_gpus": world_size, "what": label,
+            "ms_per_step": ms, "steps": steps, "n_gpus": world_size, "what": label,
             "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": gbs / HBM_PEAK_GBS, "algorithmic_bytes_per_step": nb,
                          "bytes": "552 N + 1952 W (SURVEY 8d) + 824 N: construct_obs cur/prev "
