@@ -25,9 +25,9 @@ def _snap(sim):
     return out
 
 
-def _run(sim, t0, t1):
+def _run(sim, t0, t1, write_hidden=True):
     for t in range(t0, t1):
-        sim.write_synthetic_actions(1234, t, write_hidden=True)
+        sim.write_synthetic_actions(1234, t, write_hidden=write_hidden)
         sim.step()
         sim.shift_observations()
 
@@ -53,6 +53,26 @@ def test_checkpoint_continues_bit_exactly(tmp_path, fix_depth):
     c.load_checkpoint(blob.tobytes())
     _run(c, 6, 8)
     assert c.num_agents() > 0
+
+
+@pytest.mark.gpu
+def test_checkpoint_with_aliased_action_hidden(tmp_path):
+    """Saved right after a fused shift while HiddenState was never written
+    (write_hidden=False): the current Action / HiddenState columns are views of
+    their Prev copies (DESIGN.md "Aliased current Action / HiddenState") and the
+    save copies them out; the restored manager continues bit-exactly."""
+    import madrona_bots as mb
+    a = mb.SimManager(0, 64, 13, 24)
+    _run(a, 0, 5, write_hidden=False)
+    blob = a.save_checkpoint()
+    _run(a, 5, 9, write_hidden=False)
+    ref = _snap(a)
+    b = mb.SimManager(0, 64, 13, 24)
+    b.load_checkpoint(blob.tobytes())
+    _run(b, 5, 9, write_hidden=False)
+    got = _snap(b)
+    for k in ref:
+        assert torch.equal(ref[k], got[k]), k
 
 
 @pytest.mark.gpu
