@@ -63,7 +63,8 @@ def test_checkpoint_with_aliased_action_hidden(tmp_path):
     save copies them out; the restored manager continues bit-exactly."""
     import madrona_bots as mb
     a = mb.SimManager(0, 64, 13, 24)
-    _run(a, 0, 5, write_hidden=False)
+    _run(a, 0, 3)                        # nonzero HiddenState first
+    _run(a, 3, 5, write_hidden=False)
     blob = a.save_checkpoint()
     _run(a, 5, 9, write_hidden=False)
     ref = _snap(a)
