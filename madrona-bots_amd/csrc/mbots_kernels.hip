@@ -923,7 +923,10 @@ constexpr float kFarCull = 5.0f;               // P1 angular cull from this |f| 
 
 template <int kCap>
 struct SensorLDS {
-    float2 obj[kMaxFood + kCap];              // positions: food, then agents
+    // positions: food, then agents, then (kCap <= 128) 64 NaN sentinels that P1
+    // reads past nobj unchecked (the 256-slot class keeps its bounds checks: 2 KB
+    // more per block would cost it a block per CU)
+    float2 obj[kMaxFood + kCap + (kCap <= 128 ? 64 : 0)];
     float2 frot[kMaxFood];                    // food squares' (cos, sin)
     float2 hd[kCap];                          // agent headings
     int8_t sp[kCap];
@@ -1199,6 +1202,10 @@ __global__ __launch_bounds__(64 * kSensorWorlds, kCap <= 128 ? MB_SENSOR_BLOCKS 
         c1 += __popcll(m1); c2 += __popcll(m2); c3 += __popcll(m3); c4 += __popcll(m4);
     }
     const int nobj = nf + n;
+    // sentinels past the last object: a NaN position fails every P1 test, so
+    // the pair loop needs no bounds check or clamped read (j < nobj + 63)
+    constexpr bool kPad = kCap <= 128;
+    if (kPad) L.obj[nobj + (int)lane] = make_float2(__builtin_nanf(""), __builtin_nanf(""));
     wave_sync();
 
     for (int a0 = kChunk0; a0 < n; a0 += kChunkStep) {
@@ -1218,15 +1225,15 @@ __global__ __launch_bounds__(64 * kSensorWorlds, kCap <= 128 ? MB_SENSOR_BLOCKS 
             const int self = a < nc ? nf + ia : -1;
             for (int jb = 0; jb < nobj; jb += G) {
                 const int j = jb + o;
-                // branch-free: every lane reads a valid object and masks the result
-                const float2 p = L.obj[min(j, nobj - 1)];
+                // (j >= nobj reads a NaN sentinel: keep comes out false)
+                const float2 p = L.obj[kPad ? j : min(j, nobj - 1)];
                 const float vx = p.x - ap.x, vy = p.y - ap.y;
                 // pair_fl's (f, l) up to an FMA rounding: the cull's margin
                 // (kWedge - sqrt 2 = 0.05) dwarfs it; survivors recompute exactly
                 const float f = __builtin_fmaf(vx, ah.x, vy * ah.y), l = __builtin_fmaf(vx, ah.y, -(vy * ah.x));
                 const bool food = j < nf;
                 const float af = fabsf(f);
-                bool keep = (j < nobj) & (j != self) & (a < nc) &
+                bool keep = (kPad | (j < nobj)) & (j != self) & (a < nc) &
                             (fabsf(l) <= af + (food ? kWedgeFood : kWedge));
                 {
                     // a far pair (|f| >= kFarCull) also needs a pixel centre, or

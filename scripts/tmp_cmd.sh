@@ -1,6 +1,8 @@
 #!/bin/bash
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-for r in 1 2 3 4 5; do for lib in build_var/libmbots_r0.so build_var/libmbots_cur.so; do
-  MBOTS_LIB=$lib timeout -k 10 120 python scripts/refloop.py --steps 400 || exit 1
-done; done
+mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest tests/test_parity_gpu.py -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/pytest_q.log 2>&1
+rc=$?; tail -2 gpurun_out/pytest_q.log
+if [ $rc -ne 0 ]; then grep -E "^E |Error|assert" gpurun_out/pytest_q.log | head -20; exit $rc; fi
+scripts/ab_libs.sh 4 build_var/libmbots_cur.so build_var/libmbots_nan.so -- --stream-priority -1
