@@ -1221,8 +1221,10 @@ __global__ __launch_bounds__(64 * kSensorWorlds, kCap <= 128 ? MB_SENSOR_BLOCKS 
             const int G = 64 / P, lgG = 6 - (P == 8 ? 3 : P == 4 ? 2 : P == 2 ? 1 : 0);
             const int a = (int)lane >> lgG, o = (int)lane & (G - 1);
             const int ia = a0 + min(a, nc - 1);
-            const float2 ap = L.obj[nf + ia], ah = L.hd[ia];
-            const int self = a < nc ? nf + ia : -1;
+            // a lane past the chunk's agents gets a NaN camera: every test fails
+            const float2 ap = a < nc ? L.obj[nf + ia] : make_float2(__builtin_nanf(""), __builtin_nanf(""));
+            const float2 ah = L.hd[ia];
+            const int self = nf + ia;
             for (int jb = 0; jb < nobj; jb += G) {
                 const int j = jb + o;
                 // (j >= nobj reads a NaN sentinel: keep comes out false)
@@ -1233,8 +1235,7 @@ __global__ __launch_bounds__(64 * kSensorWorlds, kCap <= 128 ? MB_SENSOR_BLOCKS 
                 const float f = __builtin_fmaf(vx, ah.x, vy * ah.y), l = __builtin_fmaf(vx, ah.y, -(vy * ah.x));
                 const bool food = j < nf;
                 const float af = fabsf(f);
-                bool keep = (kPad | (j < nobj)) & (j != self) & (a < nc) &
-                            (fabsf(l) <= af + (food ? kWedgeFood : kWedge));
+                bool keep = (kPad | (j < nobj)) & (j != self) & (fabsf(l) <= af + (food ? kWedgeFood : kWedge));
                 {
                     // a far pair (|f| >= kFarCull) also needs a pixel centre, or
                     // forward the finder ray u = 0, within w of its centre's
