@@ -1246,9 +1246,14 @@ __global__ __launch_bounds__(64 * kSensorWorlds, kCap <= 128 ? MB_SENSOR_BLOCKS 
                     const float rf = __builtin_amdgcn_rcpf(f);
                     const float uc = l * rf;
                     // (ar carries the 1.001 margin itself: every factor only grows)
+                    // The bound a (1 + u_c^2 / 2 + a |u_c|) (1 + 1.2 a^2) is taken
+                    // as a (1 + u_c^2 / 2 + a (|u_c| + 2.9 a)), never smaller where
+                    // it is used: 1.2 (1 + u_c^2 / 2 + a |u_c|) <= 2.9 for a <= 0.285
+                    // and |u_c| <= 1 + 2.06 / 5 inside the wedge (5 ops, was 8)
                     const float ar = (food ? 1.42f * 1.001f : 1.001f) * fabsf(rf);
-                    const float w = ar * __builtin_fmaf(ar, fabsf(uc), __builtin_fmaf(0.5f * uc, uc, 1.0f)) *
-                                    __builtin_fmaf(1.2f * ar, ar, 1.0f) + 1e-4f;
+                    const float w = __builtin_fmaf(
+                        ar, __builtin_fmaf(ar, __builtin_fmaf(2.9f, ar, fabsf(uc)), __builtin_fmaf(0.5f * uc, uc, 1.0f)),
+                        1e-4f);
                     const bool fwd = f > 0.0f;
                     const float sc = fwd ? 12.0f : 4.0f;
                     const float s = __builtin_fmaf(uc, sc, sc - 0.5f);
