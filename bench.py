@@ -11,9 +11,11 @@ BASELINE config 3).  Rank 0 prints one JSON line.
     python bench.py [--gpus N] [--steps K] [--warmup W] [--worlds WPG]
     torchrun --nproc-per-node N bench.py --gpus N ...
 
---gather (BASELINE config 5): every step also builds the learner observation
-rows (fused construct_obs kernel) and gathers them with the rewards to rank 0
-over RCCL (madrona-bots_amd/harness/gather.py); reported as "config5".
+With several ranks (or --gather) a second timed loop measures BASELINE config
+5: after every step each rank's rollout records (the learner's raw columns,
+64 B/agent) are gathered to rank 0 over RCCL and the [N, 69] learner rows are
+rebuilt there (madrona-bots_amd/harness/gather.py); reported as "config5".
+`python bench.py --gpus N` without a launcher starts the N ranks itself.
 
 After the main line (unless --no-secondary): the reference training loop's
 call sequence (learn/training_loop.py:36-137 without the learner math: step,
@@ -134,14 +136,17 @@ def load_profile(suffix, worlds):
     return best
 
 
-def cpu_baseline(worlds_sample, target_s):
+def cpu_baseline(worlds_sample, target_s, threads=None):
     """The build's C++ CPU restatement (SURVEY 8d "CPU baseline"): the
     product's own CPU execution mode (madrona_bots exec_mode="cpu",
     mbots_cpu.cpp: the same systems, bit-identical to the HIP path), worlds
-    split over every host thread this process is given, on a bounded sample
-    of the same workload (same seed, agents, action stream, step+shift+write)."""
+    split over `threads` host threads (default: every CPU in this process's
+    affinity set), on a bounded sample of the same workload (same seed,
+    agents, action stream, step+shift+write)."""
     import madrona_bots as mb
-    threads, aff, nproc = cpu_share()
+    share, aff, nproc = cpu_share()
+    if threads is None:
+        threads = aff
     os.environ["MBOTS_CPU_THREADS"] = str(threads)
     sim = mb.SimManager(0, worlds_sample, SEED, AGENTS_PER_WORLD, exec_mode="cpu")
     sim.write_synthetic_actions(ACTION_SEED, 0)
@@ -238,6 +243,91 @@ def reference_loop(W, args, rank, world_size, dev, distributed, label):
             "kernel_ms": ktimes}
 
 
+def spawn_ranks(args):
+    """One rank per GPU for `--gpus N` when no launcher set WORLD_SIZE: this
+    GPU-free parent runs torch.distributed.run as a child process (never an
+    exec: the children initialise the GPUs) on 127.0.0.1 and returns its exit
+    code.  Each rank then takes cuda:LOCAL_RANK (distinct devices unless
+    --same-device)."""
+    import socket
+    import subprocess
+    if not args.same_device:
+        ndev = torch.cuda.device_count()   # counts devices without creating a HIP context
+        if ndev < args.gpus:
+            print(f"bench.py: --gpus {args.gpus} needs {args.gpus} devices, {ndev} visible "
+                  "(--same-device --backend gloo rehearses several ranks on one GPU)", file=sys.stderr)
+            return 2
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr", "127.0.0.1", "--master-port", str(port),
+           os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")   # RCCL over dmabuf IPC on this host
+    return subprocess.run(cmd, env=env).returncode
+
+
+def config5_loop(mgr, args, rank, world_size, dev, distributed):
+    """BASELINE config 5: every rank steps its shard; after each step the
+    learner's reads (learn/training_loop.py:43-57, :87) travel to rank 0 as
+    64-B rollout records (harness/gather.py gather_records: RCCL gather over
+    xGMI with the nccl backend), where the [N, 69] learner rows are rebuilt by
+    the construct_obs-equivalent kernel; then shift + the learner's action
+    write.  Wall clock of the timed steps, max over ranks; returns the line's
+    dict on rank 0."""
+    import gather
+    import madrona_bots as mb
+    steps = max(10, args.steps // 2)
+    gsec = [0.0]
+    nrows = [0]
+
+    def one(t, timed):
+        mgr.step()
+        g0 = time.perf_counter()
+        if distributed:
+            out = gather.gather_records(mgr, dst=0)
+        else:   # one rank: the same records, packed and rebuilt locally
+            out = mb.unpack_rollout(mgr.pack_rollout())
+        if out is not None:
+            nrows[0] += out["obs"].shape[0] if timed else 0
+        if timed:
+            gsec[0] += time.perf_counter() - g0
+        mgr.shift_observations()
+        mgr.write_synthetic_actions(ACTION_SEED, t + 1)
+
+    t0s = args.warmup + args.steps + 100
+    for k in range(3):
+        one(t0s + k, False)
+    torch.cuda.synchronize()
+    if distributed:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(steps):
+        one(t0s + 3 + k, True)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    st = torch.tensor([el, gsec[0]], dtype=torch.float64, device=dev if args.backend == "nccl" else "cpu")
+    if distributed:
+        dist.barrier()
+        dist.all_reduce(st, op=dist.ReduceOp.MAX)
+    el, gs = float(st[0].item()), float(st[1].item())
+    if rank != 0:
+        return None
+    rows = nrows[0] / steps
+    rb = mgr.rollout_record_bytes()
+    return {"what": "step + rollout records (semantic, health, position, surrounding, reward, stats: "
+                    f"{rb} B/agent) gathered to rank 0 + [N,69] learner rows rebuilt there + shift + "
+                    "action write (harness/gather.py gather_records)",
+            "backend": args.backend if distributed else "none (one rank: pack + unpack locally)",
+            "n_gpus": world_size, "steps": steps, "ms_per_step": el / steps * 1e3,
+            "value": rows / (el / steps), "unit": "agent-steps/s (every rank's agents reaching the learner)",
+            "gather_ms_per_step": gs / steps * 1e3, "rows_per_step_at_learner": rows,
+            "gathered_bytes_per_step": rows * rb, "bytes_per_agent": rb,
+            "previous_payload_bytes_per_agent": 280}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -253,7 +343,8 @@ def main():
                     help="bracket every k-th timed step()+shift() with HIP events (roofline "
                          "launch duration); each event pair adds ~10 us of GPU idle")
     ap.add_argument("--gather", action="store_true",
-                    help="config 5: construct_obs + RCCL gather of obs/reward rows to rank 0")
+                    help="config 5 also at one rank (always run with several ranks): rollout records "
+                         "gathered to rank 0, learner rows rebuilt there")
     ap.add_argument("--backend", default="nccl",
                     help="torch.distributed backend for the bench's barrier/max/sum (nccl = RCCL); "
                          "gloo allows a rehearsal with several ranks on one GPU")
@@ -267,10 +358,24 @@ def main():
                          "faster than the caller's chain at normal (DESIGN.md 'Schedule')")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # `python bench.py --gpus N` without a launcher: start the N ranks
+        # ourselves (still GPU-free here: only device_count, no HIP context)
+        sys.exit(spawn_ranks(args))
     world_size = int(os.environ.get("WORLD_SIZE", "1"))
+    if world_size != args.gpus:
+        sys.exit(f"bench.py: WORLD_SIZE={world_size} but --gpus {args.gpus}: launch one rank per GPU "
+                 f"(torchrun --nproc-per-node {args.gpus}) or drop the launcher")
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     distributed = world_size > 1
+    if distributed and not args.same_device:
+        ndev = torch.cuda.device_count()
+        if ndev < world_size:
+            sys.exit(f"bench.py: --gpus {world_size} needs {world_size} devices, {ndev} visible "
+                     "(--same-device with --backend gloo rehearses several ranks on one GPU)")
+    if distributed and args.same_device and args.backend == "nccl":
+        sys.exit("bench.py: --same-device needs --backend gloo (RCCL takes one rank per GPU)")
     dev_index = 0 if (args.same_device or not distributed) else local_rank
     torch.cuda.set_device(dev_index)
     dev = torch.device("cuda", dev_index)
@@ -291,21 +396,8 @@ def main():
     ghost = rank < world_size - 1
     mgr = mb.SimManager(dev_index, W, SEED, AGENTS_PER_WORLD, world_offset=rank * W, shard_ghost=ghost)
 
-    gather_s = [0.0]
-
-    def learner_gather():
-        # the learner's read of this step's rows (learn/env.py:58-70) moved to rank 0
-        import gather
-        obs = mgr.construct_obs(False)
-        rew = mgr.reward_tensor(False).to_torch()
-        cnt = gather.species_rows(mgr.species_count_tensor().to_torch())
-        if distributed:
-            gather.gather_rollout({"obs": obs, "reward": rew}, cnt, dst=0)
-
     def one_step(t):
         mgr.step()
-        if args.gather:
-            learner_gather()
         mgr.shift_observations()
         mgr.write_synthetic_actions(ACTION_SEED, t + 1)
 
@@ -329,10 +421,6 @@ def main():
         if k in ev:
             ev[k][0].record()
         mgr.step()
-        if args.gather:
-            g0 = time.perf_counter()
-            learner_gather()
-            gather_s[0] += time.perf_counter() - g0
         mgr.shift_observations()
         if k in ev:
             # the span ends when both chains have: the sensor's stream joined
@@ -360,6 +448,12 @@ def main():
         torch.cuda.synchronize()
         ktimes = mgr.kernel_times()
         mgr.enable_kernel_timing(False)
+    # config 5 (BASELINE: sim + learner on rank 0, RCCL gather of the rollout
+    # tensors): its own timed loop after the main line, by default whenever the
+    # bench runs several ranks (so the driver's 1..8-GPU run covers it)
+    cfg5 = None
+    if distributed or args.gather:
+        cfg5 = config5_loop(mgr, args, rank, world_size, dev, distributed)
     secondary = ref_main = None
     if not args.no_secondary:
         secondary = reference_loop(4096, args, rank, world_size, dev, distributed,
@@ -478,16 +572,23 @@ def main():
                 if mp:
                     out["sensor_valu"]["microbench_rate"] = mp[1]
                     out["sensor_valu"]["microbench_source"] = mp[0]
-        if args.gather:
-            out["config5"] = {"what": "step + fused construct_obs + RCCL gather of obs [N,69] f32 "
-                                      "and reward rows to rank 0 (harness/gather.py) + shift",
-                              "host_gather_ms_per_step": gather_s[0] / args.steps * 1e3,
-                              "gathered_bytes_per_step": total_agent_steps / args.steps * 70 * 4}
+        if cfg5:
+            out["config5"] = cfg5
         if secondary:
             out["secondary"] = secondary
             out["reference_loop"] = ref_main
         if not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(args.cpu_worlds, args.cpu_seconds)
+            # every CPU of the affinity set ("all host cores"), on a
+            # sample of >= 64 worlds per thread; beside it the box's per-GPU
+            # share (OMP_NUM_THREADS), the pool size the box asks workers to use
+            share, aff, _ = cpu_share()
+            base = cpu_baseline(max(args.cpu_worlds, 64 * aff), args.cpu_seconds / 2, threads=aff)
+            if share != aff:
+                sh = cpu_baseline(args.cpu_worlds, args.cpu_seconds / 2, threads=share)
+                base["per_gpu_share"] = {k: sh[k] for k in ("value", "cores", "sample")}
+                base["per_gpu_share"]["note"] = ("the box's per-GPU CPU share (OMP_NUM_THREADS); "
+                                                 "the headline value uses every CPU of the affinity set")
+            out["cpu_baseline"] = base
         print(json.dumps(out), flush=True)
 
     if distributed:

@@ -140,6 +140,30 @@ int mbots_agent_offset_for_world(mbots_handle *h, uint32_t world, uint32_t *out)
 int mbots_construct_obs(mbots_handle *h, int32_t prev, float *out, uint64_t out_rows,
                         void *stream);
 
+/* Rollout records for the learner-rank gather (BASELINE config 5):
+ * the raw columns the reference's training loop reads after step()
+ * (learn/training_loop.py:43-57, :87; learn/util.py:14-29), one fixed-size
+ * record per export row, so a rank ships ~64 B per agent instead of the 276-B
+ * f32 learner row:
+ *   bytes  0..31  semantic (int8 x 32)        32..35  health (int32 bits)
+ *         36..43  position (f32 x 2)          44..51  surrounding (f32 x 2)
+ *         52..55  reward (f32)                56..59  stats (4 x uint8 flags)
+ *         60..63  zero
+ *         64..95  depth (uint8 x 32), only with MBOTS_FLAG_FIX_DEPTH_ALIAS
+ * mbots_pack_rollout writes rows [0, min(N, out_rows)) into `out` (device
+ * memory of the manager's GPU; host memory in CPU mode). */
+#define MBOTS_ROLLOUT_BYTES        64u
+#define MBOTS_ROLLOUT_BYTES_DEPTH  96u
+int mbots_rollout_record_bytes(mbots_handle *h, uint32_t *out);
+int mbots_pack_rollout(mbots_handle *h, void *out, uint64_t out_rows, void *stream);
+/* Learner side, no manager needed: `rows` gathered records (with_depth: the
+ * 96-B form) -> obs [rows, 69] f32 exactly as mbots_construct_obs builds them,
+ * reward [rows] f32 and stats [rows, 4] int32 (either may be NULL; stats
+ * 16-B aligned).  device >= 0: pointers are device memory of that GPU and the
+ * kernel runs on `stream`; device == -1: host memory, done before returning. */
+int mbots_unpack_rollout(const void *records, uint64_t rows, int32_t with_depth, int32_t device,
+                         float *obs, float *reward, int32_t *stats, void *stream);
+
 /* Checkpoint / restore (the reference has none): the live state
  * after the last step (agent SoA, RNG keys/counters, food, the current export
  * table's N rows) as a host blob.  A manager created with the same

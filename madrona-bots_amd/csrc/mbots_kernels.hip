@@ -653,6 +653,15 @@ __global__ __launch_bounds__(1024) void scan_kernel(SimState S, int parity)
     if (b == 0 && t == 0) {
         S.totals[0] = (uint32_t)s_tot[4];
         for (int k = 0; k < 4; ++k) S.totals[1 + k] = (uint32_t)s_tot[k];
+        // [5]: every table row, the shard ghost's included (they follow row N):
+        // the row moves, the shift and checkpoints carry the ghost's
+        // Action / HiddenState like every other row's
+        uint32_t rows = (uint32_t)s_tot[4];
+        if (S.W > S.Wx) {
+            const int4 g = reinterpret_cast<const int4 *>(S.scount)[S.Wx];
+            rows += (uint32_t)(g.x + g.y + g.z + g.w);
+        }
+        S.totals[kTotRows] = rows;
         *S.agent_steps += (unsigned long long)s_tot[4];
         // the host reads the row counts straight from pinned memory once the
         // event after K2 completes (no D2H copy on the step's stream)
@@ -661,6 +670,7 @@ __global__ __launch_bounds__(1024) void scan_kernel(SimState S, int parity)
             for (int k = 0; k < 5; ++k)
                 __hip_atomic_store(S.totals_host + k, k ? (uint32_t)s_tot[k - 1] : (uint32_t)s_tot[4],
                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(S.totals_host + kTotRows, rows, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             // make the mirror visible before the dispatch's completion signal,
             // whatever scope the runtime gives that signal's release
             __threadfence_system();
@@ -807,7 +817,7 @@ __device__ __forceinline__ void move_item(const MoveSeg &sg, uint32_t idx, int32
 __device__ __forceinline__ void move_rows(const uint32_t *totals, const int32_t *src_of,
                                           const MoveArgs &args)
 {
-    const uint32_t N = totals[0];
+    const uint32_t N = totals[kTotRows];   // the shard ghost's rows included
     const MoveSeg &sg = args.seg[blockIdx.y];
     const uint32_t items = N * sg.ipr;
     const uint32_t stride = gridDim.x * blockDim.x;
@@ -874,7 +884,7 @@ __global__ __launch_bounds__(256) void shift_move_kernel(const uint32_t *totals,
                                                          MoveArgs args)
 {
     const MoveSeg &sg = args.seg[blockIdx.y];
-    const uint32_t N = totals[0];
+    const uint32_t N = totals[kTotRows];
     if (sg.width == 8 && sg.ipr == 3) gather_seg<uint2, 3>(sg, N, src_of);
     else if (sg.width == 16 && sg.ipr == 4) gather_seg<uint4, 4>(sg, N, src_of);
     else if (sg.width == 16 && sg.ipr == 2) gather_seg<uint4, 2>(sg, N, src_of);
@@ -1404,6 +1414,91 @@ __global__ __launch_bounds__(256) void construct_obs_kernel(const uint32_t *tota
 }
 
 // ---------------------------------------------------------------------------
+// Rollout records for the learner-rank gather (BASELINE config 5):
+// the raw columns learn/training_loop.py:43-57 reads, 64 B per export row --
+// semantic 32 | health 4 | position 8 | surrounding 8 | reward 4 | stats as
+// four bytes 4 | pad 4 -- plus the depth bytes (96 B) when the manager fixes
+// the depth alias.  The gathered records become [N, 69] rows on the learner
+// rank (unpack_rollout_kernel: construct_obs over records, bit-identical).
+// One thread per record on the pack side (its 16-B granules are contiguous).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void pack_rollout_kernel(const uint32_t *totals, ObsTable t, int fixd,
+                                                           uint8_t *out, uint32_t out_rows)
+{
+    const uint32_t N = min(totals[0], out_rows);
+    const uint32_t rec = fixd ? kRolloutBytesDepth : kRolloutBytes;
+    for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r < N; r += gridDim.x * blockDim.x) {
+        uint4 *o = reinterpret_cast<uint4 *>(out + (size_t)r * rec);
+        const uint4 *s = reinterpret_cast<const uint4 *>(t.sem + (size_t)r * kSensor);
+        o[0] = s[0];
+        o[1] = s[1];
+        const float2 p = reinterpret_cast<const float2 *>(t.pos)[r];
+        const float2 su = reinterpret_cast<const float2 *>(t.sur)[r];
+        const int4 st = reinterpret_cast<const int4 *>(t.stats)[r];
+        const uint32_t sb = (uint32_t)(st.x & 0xFF) | (uint32_t)(st.y & 0xFF) << 8 |
+                            (uint32_t)(st.z & 0xFF) << 16 | (uint32_t)(st.w & 0xFF) << 24;
+        o[2] = make_uint4((uint32_t)t.health[r], __float_as_uint(p.x), __float_as_uint(p.y),
+                          __float_as_uint(su.x));
+        o[3] = make_uint4(__float_as_uint(su.y), __float_as_uint(t.reward[r]), sb, 0u);
+        if (fixd) {
+            const uint4 *d = reinterpret_cast<const uint4 *>(t.depth + (size_t)r * kSensor);
+            o[4] = d[0];
+            o[5] = d[1];
+        }
+    }
+}
+
+// Learner side: records -> obs [N, 69] f32 (construct_obs: depth bytes as
+// uint8 -- the semantic bytes when aliased, B.1 -- health's int32 bits as
+// f32, B.2, position, semantic as int8, surroundings), reward [N], stats
+// [N, 4] i32.  64 records per block staged in LDS, the block's 64 x 69 output
+// floats written as coalesced 16-B stores (like construct_obs_kernel).
+__global__ __launch_bounds__(256) void unpack_rollout_kernel(const uint8_t *recs, uint32_t N, int fixd,
+                                                             float *obs, float *reward, int32_t *stats)
+{
+    constexpr int kW = kRolloutBytesDepth / 16;   // granules per staged record (the widest)
+    __shared__ uint4 s_rec[kObsRows * kW];
+    const uint32_t rec = fixd ? kRolloutBytesDepth : kRolloutBytes, gpr = rec / 16;
+    const uint32_t nblk = (N + kObsRows - 1) / kObsRows;
+    const uint32_t t = threadIdx.x;
+    const uint8_t *sb = reinterpret_cast<const uint8_t *>(s_rec);
+    auto val = [&](uint32_t i) {
+        const uint32_t r = i / kObsDim, c = i - r * kObsDim;
+        const uint8_t *q = sb + (size_t)r * kW * 16;
+        if (c < 32) return (float)q[fixd ? 64 + c : c];
+        if (c < 35) return __uint_as_float(reinterpret_cast<const uint32_t *>(q)[8 + (c - 32)]);
+        if (c < 67) return (float)(int8_t)q[c - 35];
+        return __uint_as_float(reinterpret_cast<const uint32_t *>(q)[11 + (c - 67)]);
+    };
+    for (uint32_t b = blockIdx.x; b < nblk; b += gridDim.x) {
+        const uint32_t r0 = b * kObsRows, nr = min((uint32_t)kObsRows, N - r0);
+        for (uint32_t g = t; g < nr * gpr; g += 256) {
+            const uint32_t r = g / gpr, k = g - r * gpr;
+            s_rec[r * kW + k] = reinterpret_cast<const uint4 *>(recs + (size_t)r0 * rec)[g];
+        }
+        __syncthreads();
+        float *o = obs + (size_t)r0 * kObsDim;
+        if (nr == (uint32_t)kObsRows && (reinterpret_cast<uintptr_t>(obs) & 15u) == 0) {
+            for (uint32_t g = t; g < kObsRows * kObsDim / 4; g += 256)
+                reinterpret_cast<float4 *>(o)[g] = make_float4(val(4 * g), val(4 * g + 1), val(4 * g + 2),
+                                                               val(4 * g + 3));
+        } else {
+            for (uint32_t i = t; i < nr * kObsDim; i += 256) o[i] = val(i);
+        }
+        if (t < nr) {
+            const uint32_t *q = reinterpret_cast<const uint32_t *>(sb + (size_t)t * kW * 16);
+            if (reward) reward[r0 + t] = __uint_as_float(q[13]);
+            if (stats) {
+                const uint32_t s4 = q[14];
+                reinterpret_cast<int4 *>(stats)[r0 + t] =
+                    make_int4((int)(s4 & 0xFF), (int)((s4 >> 8) & 0xFF), (int)((s4 >> 16) & 0xFF), (int)(s4 >> 24));
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// ---------------------------------------------------------------------------
 // K5: shiftObservationsSystem + shiftHiddenState (sim.cpp:1002-1048): Prev* <-
 // current for rows [0, N).  Each column is a contiguous byte range, so the copy
 // is one grid-stride stream of 16-byte granules over the concatenation of the
@@ -1423,7 +1518,7 @@ __global__ __launch_bounds__(256) void construct_obs_kernel(const uint32_t *tota
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void shift_kernel(const uint32_t *totals, ObsTable t, int mode)
 {
-    const uint32_t N = totals[0];
+    const uint32_t N = totals[kTotRows];   // the shard ghost's rows included
     const bool eager = mode != kShiftRest, rest = mode != kShiftEager;
     const uint32_t g4 = rest ? (4u * N + 15u) >> 4 : 0u, g8 = rest ? (8u * N + 15u) >> 4 : 0u;
     const uint32_t g24 = eager ? (24u * N + 15u) >> 4 : 0u;
@@ -1699,6 +1794,24 @@ hipError_t launch_construct_obs(const SimState &S, const ObsTable &t, int prev, 
                        prev && !lz ? t.phealth : t.health, prev && !lz ? t.ppos : t.pos,
                        prev && !lz ? t.psur : t.sur,
                        out, out_rows);
+    return hipGetLastError();
+}
+hipError_t launch_pack_rollout(const SimState &S, const ObsTable &t, void *out, uint32_t out_rows,
+                               hipStream_t st)
+{
+    const int fixd = (S.flags & kFlagFixDepth) != 0;
+    const unsigned blocks = (unsigned)std::min<uint64_t>((out_rows + 255) / 256, 8192);
+    hipLaunchKernelGGL(pack_rollout_kernel, dim3(std::max(blocks, 1u)), dim3(256), 0, st, S.totals, t, fixd,
+                       static_cast<uint8_t *>(out), out_rows);
+    return hipGetLastError();
+}
+hipError_t launch_unpack_rollout(const void *recs, uint32_t n, int fixd, float *obs, float *reward,
+                                 int32_t *stats, hipStream_t st)
+{
+    if (n == 0) return hipSuccess;
+    const unsigned blocks = (unsigned)std::min<uint64_t>((n + kObsRows - 1) / kObsRows, 16384);
+    hipLaunchKernelGGL(unpack_rollout_kernel, dim3(blocks), dim3(256), 0, st,
+                       static_cast<const uint8_t *>(recs), n, fixd, obs, reward, stats);
     return hipGetLastError();
 }
 hipError_t launch_sensor_index(const SimState &S, int32_t *out, hipStream_t st)

@@ -30,7 +30,8 @@ struct SimState {
     int32_t *world_off;             // [W] world-major agent offsets
     int32_t *src_of;                // [W*cap] new export row -> old row (-1: new agent)
     uint32_t *overflow;             // [W] dropped births/respawns
-    uint32_t *totals;               // [0] = N, [1..4] = per-species rows
+    uint32_t *totals;               // [0] = N, [1..4] = per-species rows, [kTotRows] = table rows
+                                    // incl. the shard ghost's (after row N)
     uint32_t *totals_host;          // mapped pinned mirror of totals (written by K2)
     int32_t *tiles;                 // [2][5][ntiles][kTileBuckets] per-tile species/agent counts (K1 -> K2)
     unsigned long long *agent_steps;
@@ -61,6 +62,7 @@ struct ObsTable {
     int32_t *paction;  int32_t *pstats; float *phidden; int8_t *psem; uint8_t *pdepth;
 };
 
+constexpr int kTotRows = 5;   // totals[kTotRows]: rows the moves / shift / checkpoints cover
 uint32_t scan_tiles(uint32_t W);
 // K1 blocks add their counts into one of kTileBuckets copies of their tile's
 // counters (block index mod 8): fewer same-address atomics at K1's end
@@ -90,5 +92,11 @@ hipError_t launch_synthetic_actions(const SimState &S, const ObsTable &t, uint32
 hipError_t launch_sensor_index(const SimState &S, int32_t *out, hipStream_t st);
 hipError_t launch_construct_obs(const SimState &S, const ObsTable &t, int prev, int prev_lazy,
                                 float *out, uint32_t out_rows, hipStream_t st);
+// rollout records of the config-5 gather (MBOTS_ROLLOUT_BYTES[_DEPTH])
+constexpr uint32_t kRolloutBytes = 64, kRolloutBytesDepth = 96;
+hipError_t launch_pack_rollout(const SimState &S, const ObsTable &t, void *out, uint32_t out_rows,
+                               hipStream_t st);
+hipError_t launch_unpack_rollout(const void *recs, uint32_t n, int fixd, float *obs, float *reward,
+                                 int32_t *stats, hipStream_t st);
 
 }  // namespace mbots

@@ -18,6 +18,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstring>
 #include <memory>
@@ -80,6 +81,8 @@ struct mbots_handle {
     hipEvent_t ev_join[2] = {nullptr, nullptr};   // K3b of alternate steps done (aux)
     int last_join = -1;               // ev_join of the latest K3b, -1: none pending
     unsigned long long join_capture = 0;   // stream-capture id it was recorded in (0: none)
+    unsigned long long cap_seen = 0;  // the stream capture the last captured step belonged to
+    uint64_t cap_steps = 0;           // steps recorded into it (mbots_join wants an even count)
     // deferred K4 parts of a table half (moved from the other half along the
     // last src_of when needed): PrevAction / PrevHiddenState, the six other
     // Prev* columns (from the other half's current ones when six_lazy)
@@ -291,7 +294,7 @@ int materialize_cur_ah(mbots_handle *h, hipStream_t st, int alias_cols = 3)
     HIP_TRY(hipSetDevice(h->device));
     int rc = sync_totals(h);
     if (rc) return rc;
-    const size_t N = h->h_totals[0];
+    const size_t N = h->h_totals[mbots::kTotRows];   // the shard ghost's rows included
     const mbots::ObsTable &t = h->T[tb];
     rc = timed(h, MBOTS_TK_MOVE, st, [&] {
         hipError_t e = hipSuccess;
@@ -335,9 +338,23 @@ void note_use(mbots_handle *h, int need, int owed)
     h->forced |= need & (owed | h->prefetched);
 }
 
+// the stream the manager last launched on is being captured into a graph
+bool capturing_now(const mbots_handle *h)
+{
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    return hipStreamIsCapturing(h->last_stream, &cs) == hipSuccess && cs == hipStreamCaptureStatusActive;
+}
+
 int sync_totals(mbots_handle *h)
 {
     HIP_TRY(hipSetDevice(h->device));
+    // a host-side row count during stream capture would be the capture-time
+    // count baked into every replay (and the event wait is not capturable)
+    if (capturing_now(h))
+        return fail(MBOTS_E_INVALID,
+                    "needs the host-side agent count, which is not available while the stream is "
+                    "captured into a graph: capture only step / shift_observations / "
+                    "write_synthetic_actions / join (device-side writers), read accessors after replay");
     HIP_TRY(hipEventSynchronize(h->ev_totals));
     return MBOTS_OK;
 }
@@ -396,6 +413,45 @@ size_t ckpt_bytes(const std::vector<Seg> &v)
     for (const Seg &s : v) b += s.bytes;
     return b;
 }
+// rollout records on the host (CPU mode, and the learner side of a gather
+// that landed in host memory): the layout of include/mbots.h, the values of
+// pack_rollout_kernel / unpack_rollout_kernel (plain bit copies and the
+// uint8 / int8 -> f32 conversions of construct_obs)
+void pack_rollout_host(const int8_t *sem, const uint8_t *depth, const int32_t *health, const float *pos,
+                       const float *sur, const float *reward, const int32_t *stats, uint64_t n, uint8_t *out)
+{
+    const size_t rec = depth ? MBOTS_ROLLOUT_BYTES_DEPTH : MBOTS_ROLLOUT_BYTES;
+    for (uint64_t r = 0; r < n; ++r) {
+        uint8_t *o = out + r * rec;
+        memcpy(o, sem + r * mbots::kSensor, 32);
+        memcpy(o + 32, health + r, 4);
+        memcpy(o + 36, pos + 2 * r, 8);
+        memcpy(o + 44, sur + 2 * r, 8);
+        memcpy(o + 52, reward + r, 4);
+        for (int k = 0; k < 4; ++k) o[56 + k] = (uint8_t)stats[4 * r + k];
+        memset(o + 60, 0, 4);
+        if (depth) memcpy(o + 64, depth + r * mbots::kSensor, 32);
+    }
+}
+
+void unpack_rollout_host(const uint8_t *recs, uint64_t n, bool with_depth, float *obs, float *reward,
+                         int32_t *stats)
+{
+    const size_t rec = with_depth ? MBOTS_ROLLOUT_BYTES_DEPTH : MBOTS_ROLLOUT_BYTES;
+    for (uint64_t r = 0; r < n; ++r) {
+        const uint8_t *q = recs + r * rec;
+        float *o = obs + r * 69;
+        const uint8_t *d = with_depth ? q + 64 : q;
+        for (int c = 0; c < 32; ++c) o[c] = (float)d[c];
+        memcpy(o + 32, q + 32, 12);   // health bits, position
+        for (int c = 0; c < 32; ++c) o[35 + c] = (float)(int8_t)q[c];
+        memcpy(o + 67, q + 44, 8);    // surroundings
+        if (reward) memcpy(reward + r, q + 52, 4);
+        if (stats)
+            for (int k = 0; k < 4; ++k) stats[4 * r + k] = q[56 + k];
+    }
+}
+
 }  // namespace
 
 extern "C" {
@@ -575,6 +631,10 @@ int mbots_step(mbots_handle *h, void *stream)
     unsigned long long cap_id = 0;
     HIP_TRY(hipStreamGetCaptureInfo(st, &cap_status, &cap_id));
     const bool capturing = cap_status == hipStreamCaptureStatusActive;
+    if (capturing) {
+        if (cap_id != h->cap_seen) { h->cap_seen = cap_id; h->cap_steps = 0; }
+        ++h->cap_steps;
+    }
     if (h->last_join >= 0 && (!capturing || h->join_capture == cap_id))
         HIP_TRY(hipStreamWaitEvent(st, h->ev_join[h->last_join], 0));
     if ((rc = timed(h, MBOTS_TK_WORLD_STEP, st,
@@ -869,11 +929,66 @@ int mbots_construct_obs(mbots_handle *h, int32_t prev, float *out, uint64_t out_
     });
 }
 
+int mbots_rollout_record_bytes(mbots_handle *h, uint32_t *out)
+{
+    if (!h || !out) return fail(MBOTS_E_INVALID, "null argument");
+    *out = (h->cfg.flags & MBOTS_FLAG_FIX_DEPTH_ALIAS) ? MBOTS_ROLLOUT_BYTES_DEPTH : MBOTS_ROLLOUT_BYTES;
+    return MBOTS_OK;
+}
+
+int mbots_pack_rollout(mbots_handle *h, void *out, uint64_t out_rows, void *stream)
+{
+    if (!h || !out) return fail(MBOTS_E_INVALID, "null argument");
+    if (out_rows > 0xFFFFFFFFull) return fail(MBOTS_E_INVALID, "out_rows too large");
+    const bool fixd = (h->cfg.flags & MBOTS_FLAG_FIX_DEPTH_ALIAS) != 0;
+    if (h->cpu) {
+        const mbots::cpu::Table &t = h->cpu->table();
+        const uint64_t n = std::min<uint64_t>(h->cpu->num_agents(), out_rows);
+        pack_rollout_host(t.sem.data(), fixd ? t.depth.data() : nullptr, t.health.data(), t.pos.data(),
+                          t.sur.data(), t.reward.data(), t.stats.data(), n, static_cast<uint8_t *>(out));
+        return MBOTS_OK;
+    }
+    HIP_TRY(hipSetDevice(h->device));
+    hipStream_t st = as_stream(stream);
+    h->last_stream = st;
+    int rc = wait_sensor(h);   // the semantic / depth rows come from K3b
+    if (rc) return rc;
+    return timed(h, MBOTS_TK_OBS, st, [&] {
+        return mbots::launch_pack_rollout(h->S, h->T[h->tb], out, (uint32_t)out_rows, st);
+    });
+}
+
+int mbots_unpack_rollout(const void *records, uint64_t rows, int32_t with_depth, int32_t device, float *obs,
+                         float *reward, int32_t *stats, void *stream)
+{
+    if ((!records || !obs) && rows) return fail(MBOTS_E_INVALID, "null argument");
+    if (rows > 0xFFFFFFFFull) return fail(MBOTS_E_INVALID, "rows too large");
+    if (device < 0) {
+        unpack_rollout_host(static_cast<const uint8_t *>(records), rows, with_depth != 0, obs, reward, stats);
+        return MBOTS_OK;
+    }
+    if (stats && (reinterpret_cast<uintptr_t>(stats) & 15u))
+        return fail(MBOTS_E_INVALID, "stats must be 16-byte aligned");
+    HIP_TRY(hipSetDevice(device));
+    HIP_TRY(mbots::launch_unpack_rollout(records, (uint32_t)rows, with_depth ? 1 : 0, obs, reward, stats,
+                                         as_stream(stream)));
+    return MBOTS_OK;
+}
+
 int mbots_join(mbots_handle *h, void *stream)
 {
     if (!h) return fail(MBOTS_E_INVALID, "null handle");
     if (h->cpu) return MBOTS_OK;   // synchronous: nothing outstanding
     HIP_TRY(hipSetDevice(h->device));
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    unsigned long long cid = 0;
+    HIP_TRY(hipStreamGetCaptureInfo(as_stream(stream), &cs, &cid));
+    // the table halves and the host's deferred-move bookkeeping alternate per
+    // step: a graph of an odd number of steps would leave them out of step
+    // with the device after every replay
+    if (cs == hipStreamCaptureStatusActive && cid == h->cap_seen && (h->cap_steps & 1))
+        return fail(MBOTS_E_INVALID, "a captured sequence must hold an even number of steps (" +
+                                         std::to_string(h->cap_steps) + " recorded)");
     if (h->last_join >= 0) HIP_TRY(hipStreamWaitEvent(as_stream(stream), h->ev_join[h->last_join], 0));
     return MBOTS_OK;
 }
@@ -924,7 +1039,7 @@ int mbots_checkpoint_size(mbots_handle *h, uint64_t *out)
     }
     int rc = sync_totals(h);
     if (rc) return rc;
-    *out = ckpt_bytes(ckpt_segments(h, h->T[h->tb], h->h_totals[0]));
+    *out = ckpt_bytes(ckpt_segments(h, h->T[h->tb], h->h_totals[mbots::kTotRows]));
     return MBOTS_OK;
 }
 
@@ -945,7 +1060,7 @@ int mbots_save_checkpoint(mbots_handle *h, void *dst, uint64_t bytes)
     HIP_TRY(hipDeviceSynchronize());   // the sensor's finder / semantic rows included
     int rc = sync_totals(h);
     if (rc) return rc;
-    const uint32_t n_rows = h->h_totals[0];
+    const uint32_t n_rows = h->h_totals[mbots::kTotRows];   // the shard ghost's rows included
     const auto segs = ckpt_segments(h, h->T[h->tb], n_rows);
     const size_t need = ckpt_bytes(segs);
     if (bytes < need) return fail(MBOTS_E_INVALID, "checkpoint buffer too small");

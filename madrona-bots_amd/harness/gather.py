@@ -39,6 +39,40 @@ def reassemble(bufs, all_cnt):
     return torch.cat(parts)
 
 
+def gather_records(mgr, dst=0, group=None):
+    """Config 5 as SURVEY 8e sizes it: every rank packs its export rows'
+    raw columns into fixed rollout records (SimManager.pack_rollout: 64 B per
+    agent, 96 with real depth -- not the 276-B f32 learner rows), one padded
+    gather ships them to the learner rank, which reassembles the global
+    (species, world, slot) order and rebuilds the learner rows there with the
+    construct_obs-equivalent kernel (madrona_bots.unpack_rollout).  Returns
+    {"obs" [N, 69] f32, "reward" [N, 1] f32, "stats" [N, 4] i32} on `dst`,
+    None elsewhere; N = the rows of every rank.
+    (learn/training_loop.py:43-57, :87 -- the learner's reads after step())"""
+    import madrona_bots as mb
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    dst_global = dst if group is None else dist.get_global_rank(group, dst)
+    dev = mgr.device
+    # counts travel on the collective's device (RCCL: the GPU; gloo: host)
+    cdev = dev if dist.get_backend(group) == "nccl" else torch.device("cpu")
+    cnt = species_rows(mgr.species_count_tensor().to_torch()).to(cdev)
+    all_cnt = [torch.zeros_like(cnt) for _ in range(world)]
+    dist.all_gather(all_cnt, cnt, group=group)
+    all_cnt = torch.stack(all_cnt).cpu()
+    n_max = int(all_cnt.sum(dim=1).max())
+    rb = mgr.rollout_record_bytes()
+    pad = torch.empty((max(n_max, 1), rb), dtype=torch.uint8, device=dev)   # rows past N: padding
+    mgr.pack_rollout(pad)
+    send = pad if cdev.type == dev.type else pad.to(cdev)
+    bufs = [torch.empty_like(send) for _ in range(world)] if rank == dst else None
+    dist.gather(send, bufs, dst=dst_global, group=group)
+    if rank != dst:
+        return None
+    recs = reassemble([b[:n_max] for b in bufs], all_cnt)
+    return mb.unpack_rollout(recs.to(dev))
+
+
 def gather_rollout(tensors, rows_per_species, dst=0, group=None):
     """tensors: name -> [N_r, ...] species-major rows of this rank (same N_r);
     rows_per_species: int64 [4] summing to N_r.  Returns name -> [sum N_r, ...]

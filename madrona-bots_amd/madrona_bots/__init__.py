@@ -24,7 +24,7 @@ import types
 
 import torch  # loads the HIP runtime libmbots.so links against (same soname)
 
-__all__ = ["SimManager", "Tensor", "madrona", "ExportID", "ExecMode"]
+__all__ = ["SimManager", "Tensor", "madrona", "ExportID", "ExecMode", "unpack_rollout"]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # MBOTS_LIB: developer override to A/B alternative builds of the same library
@@ -69,6 +69,9 @@ def _load():
         "mbots_agent_offset_for_world": [vp, u32, P(u32)],
         "mbots_write_synthetic_actions": [vp, u32, u32, i32, vp],
         "mbots_join": [vp, vp],
+        "mbots_rollout_record_bytes": [vp, P(u32)],
+        "mbots_pack_rollout": [vp, vp, ctypes.c_uint64, vp],
+        "mbots_unpack_rollout": [vp, ctypes.c_uint64, i32, i32, vp, vp, vp, vp],
         "mbots_agent_steps": [vp, P(ctypes.c_uint64)],
         "mbots_overflow": [vp, P(ctypes.c_uint64)],
         "mbots_enable_kernel_timing": [vp, i32],
@@ -178,6 +181,30 @@ class Tensor:
         if t.data_ptr() != self._ptr:
             raise RuntimeError("madrona_bots: to_torch() produced a copy, expected a view")
         return t
+
+
+def unpack_rollout(records, with_depth=None):
+    """Learner side of the config-5 gather: uint8 [N, 64 | 96] rollout records
+    (SimManager.pack_rollout, gathered from every rank) -> {"obs": float32
+    [N, 69] (construct_obs, bit-identical), "reward": float32 [N, 1],
+    "stats": int32 [N, 4]} on the records' device (mbots_unpack_rollout)."""
+    if records.dtype != torch.uint8 or records.dim() != 2 or records.shape[1] not in (64, 96):
+        raise ValueError("records must be uint8 [N, 64] or [N, 96]")
+    depth = records.shape[1] == 96 if with_depth is None else bool(with_depth)
+    if depth != (records.shape[1] == 96):
+        raise ValueError("with_depth does not match the record width")
+    rec = records.contiguous()
+    n = rec.shape[0]
+    dev = rec.device
+    obs = torch.empty((n, OBS_DIM), dtype=torch.float32, device=dev)
+    rew = torch.empty((n, 1), dtype=torch.float32, device=dev)
+    st = torch.empty((n, 4), dtype=torch.int32, device=dev)
+    stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream if dev.type == "cuda" else None)
+    _check(_lib.mbots_unpack_rollout(ctypes.c_void_p(rec.data_ptr()), n, 1 if depth else 0,
+                                     dev.index if dev.type == "cuda" else -1,
+                                     ctypes.c_void_p(obs.data_ptr()), ctypes.c_void_p(rew.data_ptr()),
+                                     ctypes.c_void_p(st.data_ptr()), stream))
+    return {"obs": obs, "reward": rew, "stats": st}
 
 
 madrona = types.ModuleType("madrona_bots.madrona")
@@ -315,6 +342,30 @@ class SimManager:
         _check(_lib.mbots_construct_obs(self._h, 1 if is_prev else 0,
                                         ctypes.c_void_p(out.data_ptr()), out.shape[0],
                                         self._stream()))
+        return out[:n]
+
+    def rollout_record_bytes(self):
+        """Bytes per rollout record (include/mbots.h: 64, or 96 with real depth)."""
+        v = ctypes.c_uint32()
+        _check(_lib.mbots_rollout_record_bytes(self._h, ctypes.byref(v)))
+        return v.value
+
+    def pack_rollout(self, out=None):
+        """The raw columns the learner reads after step() (semantic, health,
+        position, surrounding, reward, stats; depth when fixed) as one uint8
+        [N, rollout_record_bytes()] record per export row -- the payload of the
+        config-5 gather to the learner rank; unpack_rollout()
+        rebuilds construct_obs rows from it.  `out` may hold more rows (padding)."""
+        import torch
+        n = self.num_agents()
+        rb = self.rollout_record_bytes()
+        if out is None:
+            out = torch.empty((n, rb), dtype=torch.uint8, device=self.device)
+        if out.dtype != torch.uint8 or out.device != self.device or not out.is_contiguous() \
+                or out.dim() != 2 or out.shape[1] != rb or out.shape[0] < n:
+            raise ValueError(f"out must be a contiguous uint8 [>= {n}, {rb}] tensor on {self.device}")
+        _check(_lib.mbots_pack_rollout(self._h, ctypes.c_void_p(out.data_ptr()), out.shape[0],
+                                       self._stream()))
         return out[:n]
 
     def save_checkpoint(self, path=None):

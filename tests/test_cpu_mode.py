@@ -177,3 +177,34 @@ def test_breed_heavy_to_capacity_256():
         mgr.shift_observations()
         orc.shift_observations()
     assert mgr.overflow() == orc.overflow() > 0
+
+
+@pytest.mark.gpu
+def test_shard_ghost_learner_actions_cpu_equals_hip():
+    """A shard with a ghost world (MBOTS_FLAG_SHARD_GHOST) driven by a learner
+    writing Action / HiddenState through the exported views (the reference
+    loop, learn/training_loop.py:136-137): the ghost's rows are never written
+    by the learner (it only sees rows [0, N)), so they carry their last actions
+    through the row moves and the shift -- identically in both execution modes
+    (the HIP moves used to stop at row N)."""
+    import madrona_bots as mb
+    W = 48
+    h = mb.SimManager(0, W, 69, 32, shard_ghost=True)
+    c = _mgr(W, shard_ghost=True)
+    for m in (h, c):
+        m.write_synthetic_actions(1234, 0, True)   # every row, the ghost's included
+    for t in range(10):
+        for m in (h, c):
+            m.step()
+        _same(h, c, f"step {t}")
+        for m in (h, c):
+            m.shift_observations()
+        n = h.num_agents()
+        g = torch.Generator().manual_seed(77 + t)
+        a = torch.zeros((n, 6), dtype=torch.int32)
+        a[torch.arange(n), torch.randint(0, 6, (n,), generator=g)] = 1
+        hid = torch.rand((n, 16), generator=g)
+        for m in (h, c):
+            m.action_tensor(False).to_torch().copy_(a)
+            m.hidden_state_tensor(False).to_torch().copy_(hid)
+        _same(h, c, f"write {t}")

@@ -71,3 +71,58 @@ def test_gather_two_shards_equals_one():
         assert p.exitcode == 0
     ok = q.get(timeout=5)
     assert all(ok.values()), ok
+
+
+def _records_worker(rank, world, port, q, fix_depth):
+    sys.path[:0] = [HARNESS, os.path.join(ROOT, "madrona-bots_amd")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import gather
+        import madrona_bots as mb
+        kw = dict(exec_mode="cpu", fix_depth_alias=fix_depth)
+
+        def run(m):
+            for t in range(STEPS):
+                m.write_synthetic_actions(1234, t, True)
+                m.step()
+                if t < STEPS - 1:
+                    m.shift_observations()
+
+        # faithful B.3 rewards: every shard but the last steps the shard ghost
+        sim = mb.SimManager(0, W, SEED, 32, world_offset=rank * W, shard_ghost=rank < world - 1, **kw)
+        run(sim)
+        out = gather.gather_records(sim, dst=0)
+        if rank == 0:
+            full = mb.SimManager(0, world * W, SEED, 32, **kw)
+            run(full)
+            ref = {"obs": full.construct_obs(False), "reward": full.reward_tensor(False).to_torch(),
+                   "stats": full.stats_tensor(False).to_torch()}
+            q.put({k: torch.equal(out[k].view(torch.int32), ref[k].contiguous().view(torch.int32))
+                   for k in ref})
+        else:
+            assert out is None
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("fix_depth", [False, True])
+def test_gather_records_two_cpu_shards_equal_one(fix_depth):
+    """Config 5 as SURVEY 8e sizes it: 64-B (96-B with real depth) rollout
+    records from two CPU-mode shards gathered over gloo, the [N, 69] learner
+    rows rebuilt on rank 0 == one manager's construct_obs bitwise, with its
+    rewards (faithful B.3 through the shard ghost) and stats."""
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_records_worker, args=(r, 2, port, q, fix_depth)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=240)
+        assert p.exitcode == 0
+    ok = q.get(timeout=5)
+    assert all(ok.values()), ok

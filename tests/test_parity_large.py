@@ -156,3 +156,48 @@ def test_config5_gather_reassembly_on_device():
             bufs.append(pad)
         got = gather.reassemble(bufs, all_cnt)
         assert torch.equal(got.view(torch.uint8), want[name].view(torch.uint8)), name
+
+
+@pytest.mark.parametrize("fix_depth", [False, True])
+def test_config5_rollout_records_two_shards_equal_one(fix_depth):
+    """Config 5 payload: two HIP shards (faithful B.3 rewards, the
+    first with the shard ghost) pack 64-B (96-B) rollout records on device;
+    the learner-side reassembly + unpack_rollout kernel rebuild [N, 69] rows,
+    rewards and stats bit-identical to one manager holding both shards."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "madrona-bots_amd", "harness"))
+    import gather
+    import madrona_bots as mb
+    W = 1024
+
+    def run(m):
+        for t in range(6):
+            m.write_synthetic_actions(1234, t, True)
+            m.step()
+            if t < 5:
+                m.shift_observations()
+
+    full = mb.SimManager(0, 2 * W, 69, 32, fix_depth_alias=fix_depth)
+    run(full)
+    shards = [mb.SimManager(0, W, 69, 32, fix_depth_alias=fix_depth, world_offset=r * W,
+                            shard_ghost=r == 0) for r in range(2)]
+    for s in shards:
+        run(s)
+    rows = [gather.species_rows(s.species_count_tensor().to_torch()) for s in shards]
+    all_cnt = torch.stack([r.cpu() for r in rows])
+    n_max = int(all_cnt.sum(1).max())
+    rb = shards[0].rollout_record_bytes()
+    assert rb == (96 if fix_depth else 64)
+    bufs = []
+    for s in shards:
+        pad = torch.full((n_max, rb), 0xAB, dtype=torch.uint8, device="cuda")
+        s.pack_rollout(pad)
+        bufs.append(pad)
+    got = mb.unpack_rollout(gather.reassemble(bufs, all_cnt))
+    want = {"obs": full.construct_obs(False), "reward": full.reward_tensor(False).to_torch(),
+            "stats": full.stats_tensor(False).to_torch()}
+    for k in want:
+        assert torch.equal(got[k].view(torch.int32), want[k].contiguous().view(torch.int32)), k
+    # the records hold what the learner needs at 64 B/agent against 280 B of f32 rows + reward
+    assert full.pack_rollout().numel() == full.num_agents() * rb
