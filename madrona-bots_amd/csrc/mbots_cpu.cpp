@@ -440,6 +440,10 @@ void Sim::sensor_world(uint32_t w, Table &nxt)
     }
     thread_local std::vector<float2> hd;
     hd.resize(cap_);
+    // every ray's near point (nearSphere, mgr.cpp:133); the finder's at u = 0
+    NearPt np[kRays];
+    for (int k = 0; k < kSensor; ++k) np[k] = near_pt(ray_u(k));
+    np[kSensor] = finder_np();
     for (int i = 0; i < n; ++i) heading(rw_[base + i], rz_[base + i], hd[i].x, hd[i].y);
     for (int i = 0; i < n; ++i) {
         const float ax = x_[base + i], ay = y_[base + i];
@@ -458,32 +462,47 @@ void Sim::sensor_world(uint32_t w, Table &nxt)
             const uint32_t order = kOrderFood + (uint32_t)j;
             for (int k = 0; k < kSensor; ++k) {
                 const bool fwd = k < 24;
-                if (box_hit(b, ray_u(k), fwd)) key[k] = std::min(key[k], zkey(box_z(b, fwd), order));
+                if (box_hit(b, ray_u(k), fwd, np[k].c)) key[k] = std::min(key[k], zkey(box_z(b, fwd), order));
             }
-            if (box_hit(b, 0.0f, true)) key[kSensor] = std::min(key[kSensor], zkey(box_z(b, true), order));
+            if (box_hit(b, 0.0f, true, np[kSensor].c))
+                key[kSensor] = std::min(key[kSensor], zkey(box_z(b, true), order));
         }
         for (int j = 0; j < n; ++j) {
             if (j == i) continue;
             float f, l;
             fl_of(x_[base + j], y_[base + j], f, l);
             const uint32_t order = kOrderAgent + (uint32_t)j;
-            for (int k = 0; k < kSensor; ++k) key[k] = std::min(key[k], pixel_key(f, l, ray_u(k), k < 24, order));
+            for (int k = 0; k < kSensor; ++k)
+                key[k] = std::min(key[k], pixel_key(f, l, ray_u(k), np[k], k < 24, order));
             key[kSensor] = std::min(key[kSensor], finder_key(f, l, order));
         }
+        // each ray's near point: in the inner rectangle (the wall is the exit
+        // from it), inside a wall box (the wall, at s0) or beyond (a miss)
+        auto cls_of = [&](int k, bool fwd) {
+            const float ex = np[k].c * h.x + np[k].s * h.y, ey = np[k].c * h.y + np[k].s * (-h.x);
+            return wall_class(fwd ? ax + ex : ax - ex, fwd ? ay + ey : ay - ey);
+        };
         const size_t r = (size_t)obsrow_[base + i];
         for (int k = 0; k < kSensor; ++k) {
-            const float u = ray_u(k), sgn = k < 24 ? 1.0f : -1.0f;
+            const bool fwd = k < 24;
+            const float u = ray_u(k), sgn = fwd ? 1.0f : -1.0f;
             const float dx = sgn * (h.x + u * h.y), dy = sgn * (h.y + u * (-h.x));
             const uint32_t kv = key[k];
             const float oz = u2f(kv & ~kOrderMask);
             const uint32_t order = kv & kOrderMask;
-            const bool obj = (kv != kNoKey) && beats_wall(ax, ay, dx, dy, oz);
-            nxt.sem[r * kSensor + k] =
-                (int8_t)(obj ? (order < kOrderAgent ? 6 : species_[base + order - kOrderAgent]) : 5);
-            if (fixd) nxt.depth[r * kSensor + k] = depth_u8(obj ? oz : wall_z(ax, ay, dx, dy));
+            const int cls = cls_of(k, fwd);
+            const bool obj = (kv != kNoKey) && (cls == kWallInner ? beats_wall(ax, ay, dx, dy, oz) : cls == kWallNone);
+            nxt.sem[r * kSensor + k] = (int8_t)(obj ? (order < kOrderAgent ? 6 : species_[base + order - kOrderAgent])
+                                                    : (cls == kWallNone ? -1 : 5));
+            if (fixd)
+                nxt.depth[r * kSensor + k] = depth_u8(obj ? oz
+                                                      : cls == kWallInner ? wall_z(ax, ay, dx, dy)
+                                                      : cls == kWallBox ? np[k].c : __builtin_inff());
         }
         const uint32_t kv = key[kSensor], order = kv & kOrderMask;
-        const bool agent = kv != kNoKey && order >= kOrderAgent && beats_wall(ax, ay, h.x, h.y, u2f(kv & ~kOrderMask));
+        const int fcls = cls_of(kSensor, true);
+        const bool agent = kv != kNoKey && order >= kOrderAgent &&
+                           (fcls == kWallInner ? beats_wall(ax, ay, h.x, h.y, u2f(kv & ~kOrderMask)) : fcls == kWallNone);
         finder_[base + i] = agent ? (int32_t)(order - kOrderAgent) : -1;
     }
 }

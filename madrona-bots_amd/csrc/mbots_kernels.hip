@@ -921,14 +921,17 @@ __global__ __launch_bounds__(256) void shift_move_kernel(const uint32_t *totals,
 constexpr int kKeyAgents = MB_KEY_AGENTS;     // agents per chunk (key rows)
 constexpr int kKeyStride = 36;                // key row: 32 pixels, finder, pad (16-B rows)
 constexpr int kQueueCap = 128;                // P1 survivors (flushed at >= 64)
-constexpr float kWedge = 1.41421356f + 0.05f; // |l| <= |f| + sqrt(2): necessary for |u| < 1
+// |l| <= |f| + R sqrt(2): necessary for a radius-R disc on a ray |u| < 1
+constexpr float kWedge = 1.41421356f * kAgentR + 0.05f;
 constexpr float kUEps = 2e-3f;                // root-interval margin in u
 // food squares lie inside their circumscribed circle, radius sqrt 2 (1.42 with
 // margin): the wedge |l| <= |f| + sqrt(2) 1.42; candidate pixels from the
-// corner slopes when |f| > kFoodFar (the square then lies wholly on one side
-// of the camera plane), every ray exactly (the wide list) otherwise
+// corner slopes when |f| > kFoodFar (the square then lies wholly beyond the
+// near sphere, on one side of the camera plane), every ray exactly (the wide
+// list) otherwise; discs likewise beyond kCircleFar (> 1.1 + 0.92)
 constexpr float kWedgeFood = 1.41421356f * 1.42f + 0.05f;
-constexpr float kFoodFar = 2.5f;
+constexpr float kFoodFar = 2.6f;
+constexpr float kCircleFar = 2.05f;
 constexpr float kFarCull = 5.0f;               // P1 angular cull from this |f| on
 
 template <int kCap>
@@ -977,6 +980,10 @@ template <class LDS>
 __device__ __forceinline__ void run_wide(LDS &L, int nf, int a0, int q0, int cnt)
 {
     const int lane = (int)__lane_id();
+    // ray k's offset and near point (the near sphere): loop invariant
+    const int k = lane & 31;
+    const float uk = L.u[k];
+    const NearPt np = near_pt(uk), fnp = finder_np();
     for (int e0 = 0; e0 < cnt; e0 += 2) {
         const int e = e0 + (lane >> 5);
         if (e < cnt) {
@@ -986,14 +993,13 @@ __device__ __forceinline__ void run_wide(LDS &L, int nf, int a0, int q0, int cnt
             uint32_t order;
             pair_fl(L, nf, a0 + ic, j, f, l, order);
             uint32_t *kr = L.key + ic * kKeyStride;
-            const int k = lane & 31;
             uint32_t kv, kf;
             if (j < nf) {   // food square: every ray exactly
                 const FoodBox b = box_setup(f, l, L.frot[j], L.hd[a0 + ic]);
-                kv = box_hit(b, L.u[k], k < 24) ? zkey(box_z(b, k < 24), order) : kNoKey;
-                kf = box_hit(b, 0.0f, true) ? zkey(box_z(b, true), order) : kNoKey;
+                kv = box_hit(b, uk, k < 24, np.c) ? zkey(box_z(b, k < 24), order) : kNoKey;
+                kf = box_hit(b, 0.0f, true, fnp.c) ? zkey(box_z(b, true), order) : kNoKey;
             } else {
-                kv = pixel_key(f, l, L.u[k], k < 24, order);
+                kv = pixel_key(f, l, uk, np, k < 24, order);
                 kf = finder_key(f, l, order);
             }
             if (kv != kNoKey) atomicMin(&kr[k], kv);
@@ -1019,14 +1025,15 @@ __device__ __forceinline__ void run_survivors(LDS &L, int nf, int a0, int q0, in
         pair_fl(L, nf, a0 + ic, j, f, l, order);
         const bool food = j < nf;
         const float r2 = f * f + l * l;
-        if (food ? fabsf(f) <= kFoodFar : (r2 <= 1.0f) | (fabsf(f) <= 1.5f)) {
+        if (fabsf(f) <= (food ? kFoodFar : kCircleFar)) {
             wide = true;
         } else {
-            // A far pair: the object lies wholly on one side of the camera
-            // plane (circle: |f| > 1.5; square: |f| > 2.5 > its half-diagonal
-            // 1.42, so every corner has |X| >= 1.08).  Its hit interval in u,
-            // approximately: the circle's roots (lf -+ sqrt(r^2 - 1)) / (f^2 - 1),
-            // or the square's extreme corner slopes Y / X.
+            // A far pair: the object lies wholly beyond the near sphere, on one
+            // side of the camera plane (circle: |f| > 2.05 > 1.1 + 0.92; square:
+            // |f| > 2.6 > 1.1 + its half-diagonal 1.42, so every corner has
+            // |X| >= 1.18).  Its hit interval in u, approximately: the circle's
+            // roots (lf -+ sqrt(r^2 - R^2)) / (f^2 - R^2), or the square's
+            // extreme corner slopes Y / X.
             const bool fwd = f > 0.0f;
             const float sc = fwd ? 12.0f : 4.0f;
             float ulo, uhi;
@@ -1042,8 +1049,8 @@ __device__ __forceinline__ void run_survivors(LDS &L, int nf, int a0, int q0, in
                 ulo = fminf(fminf(s0, s1), fminf(s2, s3));
                 uhi = fmaxf(fmaxf(s0, s1), fmaxf(s2, s3));
             } else {
-                const float sq = __builtin_amdgcn_sqrtf(r2 - 1.0f);
-                const float ia = __builtin_amdgcn_rcpf(f * f - 1.0f);
+                const float sq = __builtin_amdgcn_sqrtf(r2 - kAgentR2);
+                const float ia = __builtin_amdgcn_rcpf(f * f - kAgentR2);
                 const float lf = l * f;
                 ulo = (lf - sq) * ia;
                 uhi = (lf + sq) * ia;
@@ -1063,8 +1070,9 @@ __device__ __forceinline__ void run_survivors(LDS &L, int nf, int a0, int q0, in
             // u) inside the true interval, where the approximate bounds are off
             // by ~1e-6: for a circle the float q(u) is then off by < 1e-4 of a
             // value <= -0.08; for a square every corner's S = Y - u X is
-            // >= 1.08 x 0.08 from 0 (|X| >= 1.08), against a float error of the
-            // line test < 1e-4.  They are hits carrying the object's key.
+            // >= 1.18 x 0.08 from 0 (|X| >= 1.18), against a float error of the
+            // line test < 1e-4.  They are hits carrying the object's key (a far
+            // object lies beyond the near sphere: nothing of it is clipped).
             const int kl = k0 + max(c - 1, 0);
             const float ua = L.u[k0 & 31], ub = L.u[kl & 31];
             bool ha, hb, hf;
@@ -1077,9 +1085,9 @@ __device__ __forceinline__ void run_survivors(LDS &L, int nf, int a0, int q0, in
             } else {
                 ha = far_pixel_hit(f, l, ua, fwd);
                 hb = far_pixel_hit(f, l, ub, fwd);
-                // finder ray (u = 0) of a far pair: q(0) = l^2 - 1 <= 0 and f > 0
-                hf = (l * l - 1.0f <= 0.0f) & fwd;
-                kin = zkey(fwd ? f - 1.0f : -f - 1.0f, order);
+                // finder ray (u = 0) of a far pair: q(0) = l^2 - R^2 <= 0 and f > 0
+                hf = (l * l - kAgentR2 <= 0.0f) & fwd;
+                kin = zkey(fwd ? f - kAgentR : -f - kAgentR, order);
             }
             if ((c > 0) & ha) atomicMin(&kr[k0], kin);
             if ((c > 1) & hb) atomicMin(&kr[kl], kin);
@@ -1260,7 +1268,7 @@ __global__ __launch_bounds__(64 * kSensorWorlds, kCap <= 128 ? MB_SENSOR_BLOCKS 
                     // as a (1 + u_c^2 / 2 + a (|u_c| + 2.9 a)), never smaller where
                     // it is used: 1.2 (1 + u_c^2 / 2 + a |u_c|) <= 2.9 for a <= 0.285
                     // and |u_c| <= 1 + 2.06 / 5 inside the wedge (5 ops, was 8)
-                    const float ar = (food ? 1.42f * 1.001f : 1.001f) * fabsf(rf);
+                    const float ar = (food ? 1.42f * 1.001f : kAgentR * 1.001f) * fabsf(rf);
                     const float w = __builtin_fmaf(
                         ar, __builtin_fmaf(ar, __builtin_fmaf(2.9f, ar, fabsf(uc)), __builtin_fmaf(0.5f * uc, uc, 1.0f)),
                         1e-4f);
@@ -1309,9 +1317,15 @@ __global__ __launch_bounds__(64 * kSensorWorlds, kCap <= 128 ? MB_SENSOR_BLOCKS 
             // backward pixels look along -(h + u r): the sign folded into the
             // heading, sgn (h.x + u h.y) == (sgn h.x) + u (sgn h.y) exactly (IEEE
             // rounding is sign-symmetric)
-            const float hxs = g < 6 ? h.x : -h.x, hys = g < 6 ? h.y : -h.y;
+            const bool fw = g < 6;
+            const float hxs = fw ? h.x : -h.x, hys = fw ? h.y : -h.y;
             const uint32_t kvs[4] = {kv4.x, kv4.y, kv4.z, kv4.w};
             const float us[4] = {u4.x, u4.y, u4.z, u4.w};
+            // an agent 1.2 inside the inner rectangle has every ray's near point
+            // (1.1 from it) in the rectangle: the wall is the exit from it.  The
+            // others place each near point: inner / in a wall box / beyond.
+            const bool deep = (p.x >= kInLo + 1.2f) & (p.x <= kInHiX - 1.2f) & (p.y >= kInLo + 1.2f) &
+                              (p.y <= kInHiY - 1.2f);
             uint32_t semv = 0, depv = 0;
 #pragma unroll
             for (int t = 0; t < 4; ++t) {
@@ -1320,13 +1334,24 @@ __global__ __launch_bounds__(64 * kSensorWorlds, kCap <= 128 ? MB_SENSOR_BLOCKS 
                 const uint32_t kv = kvs[t];
                 const float oz = __uint_as_float(kv & ~kOrderMask);
                 const uint32_t order = kv & kOrderMask;
-                const bool obj = (kv != kNoKey) & beats_wall(p.x, p.y, dx, dy, oz);
+                int cls = kWallInner;
+                float s0 = 0.0f;
+                if (!deep) {
+                    const NearPt np = near_pt(u);
+                    const float ex = np.c * h.x + np.s * h.y, ey = np.c * h.y + np.s * (-h.x);
+                    cls = wall_class(fw ? p.x + ex : p.x - ex, fw ? p.y + ey : p.y - ey);
+                    s0 = np.c;
+                }
+                const bool obj = (kv != kNoKey) &
+                                 (cls == kWallInner ? beats_wall(p.x, p.y, dx, dy, oz) : cls == kWallNone);
                 // (any index in range: the species is used only for an agent's order)
                 const int spv = (int)L.sp[(order - kOrderAgent) & (kCap - 1)];
-                const int sem = obj ? (order < kOrderAgent ? 6 : spv) : 5;
+                const int sem = obj ? (order < kOrderAgent ? 6 : spv) : (cls == kWallNone ? -1 : 5);
                 semv |= (uint32_t)(uint8_t)(int8_t)sem << (8 * t);
                 if (depth) {
-                    const float z = obj ? oz : wall_z(p.x, p.y, dx, dy);
+                    const float z = obj ? oz
+                                  : cls == kWallInner ? wall_z(p.x, p.y, dx, dy)
+                                  : cls == kWallBox ? s0 : __builtin_inff();
                     depv |= (uint32_t)depth_u8(z) << (8 * t);
                 }
             }
@@ -1341,8 +1366,12 @@ __global__ __launch_bounds__(64 * kSensorWorlds, kCap <= 128 ? MB_SENSOR_BLOCKS 
             const float2 p = L.obj[nf + i], h = L.hd[i];
             const uint32_t kv = L.key[lane * kKeyStride + kSensor];
             const uint32_t order = kv & kOrderMask;
+            const NearPt fnp = finder_np();
+            const float ex = fnp.c * h.x + fnp.s * h.y, ey = fnp.c * h.y + fnp.s * (-h.x);
+            const int cls = wall_class(p.x + ex, p.y + ey);
             const bool agent = (kv != kNoKey) & (order >= kOrderAgent) &&
-                               beats_wall(p.x, p.y, h.x, h.y, __uint_as_float(kv & ~kOrderMask));
+                               (cls == kWallInner ? beats_wall(p.x, p.y, h.x, h.y, __uint_as_float(kv & ~kOrderMask))
+                                                  : cls == kWallNone);
             S.finder[base + i] = agent ? (int32_t)(order - kOrderAgent) : -1;
         }
         wave_sync();

@@ -18,12 +18,38 @@ constexpr uint32_t kOrderMask = 0x1FFu;
 constexpr float kInLo = 0.0f + 0.2f;          // inner arena rectangle (walls, sim.cpp:157-194)
 constexpr float kInHiX = 128.0f - 0.2f;
 constexpr float kInHiY = 96.0f - 0.2f;
+constexpr float kOutLo = 0.0f - 0.2f;         // the wall boxes' outer faces
+constexpr float kOutHiX = 128.0f + 0.2f;
+constexpr float kOutHiY = 96.0f + 0.2f;
+// rays see only what lies beyond nearSphere from the camera at the agent's
+// centre (mgr.cpp:133; attachEntityToView offset {0,0,0}, sim.cpp:221)
+constexpr float kNearSphere = 1.1f;
+// other agents: discs of agent_render.obj's cross-section in the rays' plane
+// (the mesh's z = 0 section: radii 0.910-0.921)
+constexpr float kAgentR = 0.92f;
+constexpr float kAgentR2 = 0.8464f;           // kAgentR^2
 
 MB_HD float max0(float x) { return x > 0.0f ? x : 0.0f; }
 MB_HD float zq(float z) { return u2f(f2u(z) & ~kOrderMask); }
 MB_HD uint32_t zkey(float z, uint32_t order)
 {
     return (f2u(z) & ~kOrderMask) | order;
+}
+
+// ray k's near point in the agent frame, (c, s) = 1.1 (1, u) / sqrt(1 + u^2)
+// (c is also the ray parameter s0 of that point along (1, u)), and
+// e = 1.1 sqrt(1 + u^2); the oracle's near_pt
+struct NearPt {
+    float c, s, e;
+};
+MB_HD NearPt near_pt(float u)
+{
+    const float n = sqrtf(1.0f + u * u);
+    NearPt r;
+    r.c = kNearSphere / n;
+    r.s = u * r.c;
+    r.e = kNearSphere * n;
+    return r;
 }
 
 // predicates below use non-short-circuit & | so they compile to VALU selects,
@@ -33,10 +59,19 @@ MB_HD bool inside_arena(float ox, float oy)
     return (ox >= kInLo) & (ox <= kInHiX) & (oy >= kInLo) & (oy <= kInHiY);
 }
 
-// wall depth of a ray: exit from the inner rectangle; 0 inside a wall box
+// inside one of the four wall boxes (sim.cpp:168-180)
+MB_HD bool in_wall_box(float x, float y)
+{
+    const bool xs = (x >= 0.0f) & (x <= 128.0f), ys = (y >= 0.0f) & (y <= 96.0f);
+    const bool bx = ((x >= kOutLo) & (x <= kInLo)) | ((x >= kInHiX) & (x <= kOutHiX));
+    const bool by = ((y >= kOutLo) & (y <= kInLo)) | ((y >= kInHiY) & (y <= kOutHiY));
+    return (bx & ys) | (by & xs);
+}
+
+// wall depth of a ray whose near point lies in the inner rectangle: its exit
+// from the rectangle along (dx, dy) from the origin
 MB_HD float wall_z(float ox, float oy, float dx, float dy)
 {
-    if (!inside_arena(ox, oy)) return 0.0f;
     float tx = __builtin_inff(), ty = __builtin_inff();
     if (dx > 0.0f) tx = (kInHiX - ox) / dx;
     else if (dx < 0.0f) tx = (kInLo - ox) / dx;
@@ -53,7 +88,15 @@ MB_HD bool beats_wall(float ox, float oy, float dx, float dy, float z)
 {
     const bool bx = (dx == 0.0f) | (z * fabsf(dx) < (dx > 0.0f ? kInHiX - ox : ox - kInLo));
     const bool by = (dy == 0.0f) | (z * fabsf(dy) < (dy > 0.0f ? kInHiY - oy : oy - kInLo));
-    return inside_arena(ox, oy) & bx & by;
+    return bx & by;
+}
+
+// where a ray's near point P0 lies: the inner rectangle (the wall is the exit
+// from it), inside a wall box (the wall, at s0), or beyond the walls (a miss)
+constexpr int kWallInner = 0, kWallBox = 1, kWallNone = 2;
+MB_HD int wall_class(float px, float py)
+{
+    return inside_arena(px, py) ? kWallInner : in_wall_box(px, py) ? kWallBox : kWallNone;
 }
 
 MB_HD uint32_t order_of(int nf, int j)
@@ -61,38 +104,41 @@ MB_HD uint32_t order_of(int nf, int j)
     return j < nf ? kOrderFood + (uint32_t)j : kOrderAgent + (uint32_t)(j - nf);
 }
 
-// exact predicate of (f, l) on pixel ray k < 32 with offset u; key or kNoKey
-MB_HD uint32_t pixel_key(float f, float l, float u, bool fwdk, uint32_t order)
+// Exact predicate of a radius-R circle at (f, l) on ray (1, u) (fwdk) or
+// -(1, u): the line meets it iff q(u) = (A u - 2 l f) u + C <= 0
+// (A = f^2 - R^2, C = l^2 - R^2); the ray leaves it beyond the near sphere iff
+// the near point lies inside it or the chord's midpoint lies beyond the near
+// point (+-p >= e, p = f + u l).  Key (depth f - R, backward -f - R) or kNoKey.
+MB_HD uint32_t pixel_key(float f, float l, float u, const NearPt &np, bool fwdk, uint32_t order)
 {
-    const float A = f * f - 1.0f, B2 = 2.0f * (l * f), C = l * l - 1.0f;
+    const float A = f * f - kAgentR2, B2 = 2.0f * (l * f), C = l * l - kAgentR2;
     const float q = (A * u - B2) * u + C;
     const float p = f + u * l;
-    // ahead of the camera: p > 0 (forward) / p < 0 (backward), i.e. (+-p) > 0
-    const bool hit = (q <= 0.0f) & ((fwdk ? p : -p) > 0.0f);
-    const float z = zq(max0(fwdk ? f - 1.0f : -f - 1.0f));
-    const bool near = f * f + l * l <= 1.0f;
-    const uint32_t key = zkey(near ? 0.0f : z, order);
-    return (hit | near) ? key : kNoKey;
+    const float nx = fwdk ? np.c - f : -np.c - f, ny = fwdk ? np.s - l : -np.s - l;
+    const bool in0 = nx * nx + ny * ny <= kAgentR2;
+    const bool hit = in0 | ((q <= 0.0f) & ((fwdk ? p : -p) >= np.e));
+    const uint32_t key = zkey(zq(max0(fwdk ? f - kAgentR : -f - kAgentR)), order);
+    return hit ? key : kNoKey;
 }
 
-// pixel_key's hit test for a far pair (f^2 + l^2 > 1, |f| > 1.5: never "near";
-// its key is zkey(fwd ? f - 1 : -f - 1, order) on every pixel it hits)
+// pixel_key's hit test for a far pair (|f| > kCircleFar: the circle lies
+// wholly beyond the near sphere, on one side of the camera plane, so in0 is
+// false and +-p >= e reduces to +-p > 0 wherever q <= 0; its key is that of
+// pixel_key on every pixel it hits)
 MB_HD bool far_pixel_hit(float f, float l, float u, bool fwdk)
 {
-    const float A = f * f - 1.0f, B2 = 2.0f * (l * f), C = l * l - 1.0f;
+    const float A = f * f - kAgentR2, B2 = 2.0f * (l * f), C = l * l - kAgentR2;
     const float q = (A * u - B2) * u + C;
     const float p = f + u * l;
     return (q <= 0.0f) & ((fwdk ? p : -p) > 0.0f);
 }
 
-// the finder ray (u = 0)
+// the finder ray (u = 0, forward; near point (1.1, 0), e = 1.1): pixel_key's
+// expressions at u = 0 (the oracle evaluates the generic form there)
+MB_HD NearPt finder_np() { return near_pt(0.0f); }
 MB_HD uint32_t finder_key(float f, float l, uint32_t order)
 {
-    const float C = l * l - 1.0f;
-    const bool hit = (C <= 0.0f) & (f > 0.0f);
-    const bool near = f * f + l * l <= 1.0f;
-    const uint32_t key = zkey(near ? 0.0f : zq(max0(f - 1.0f)), order);
-    return (hit | near) ? key : kNoKey;
+    return pixel_key(f, l, 0.0f, finder_np(), true, order);
 }
 
 // ---------------------------------------------------------------------------
@@ -158,20 +204,27 @@ MB_HD bool box_finder_hit(const FoodBox &b)
     return fabsf(b.l) <= fabsf(b.q) + fabsf(b.p);
 }
 
+// slab of one box axis along (1, u): lower / upper end of the ray parameter
 MB_HD float slab_lo(float m, float b)
 {
     return b > 0.0f ? (m - 1.0f) / b : b < 0.0f ? (m + 1.0f) / b : -__builtin_inff();
 }
+MB_HD float slab_hi(float m, float b)
+{
+    return b > 0.0f ? (m + 1.0f) / b : b < 0.0f ? (m - 1.0f) / b : __builtin_inff();
+}
 
-MB_HD bool box_hit(const FoodBox &b, float u, bool fwd)
+// the line test, then the ray's exit from the square beyond the near sphere:
+// forward hi >= s0, backward lo <= -s0, [lo, hi] the slabs' parameter interval
+// (box coordinates s b_i - m_i: m1 = f p + l q, m2 = l p - f q, b1 = p + u q,
+// b2 = u p - q); s0 = NearPt.c
+MB_HD bool box_hit(const FoodBox &b, float u, bool fwd, float s0)
 {
     if (!box_line_hit(b, u)) return false;
-    if (b.f - b.ext > 0.0f) return fwd;
-    if (b.f + b.ext < 0.0f) return !fwd;
     const float m1 = b.f * b.p + b.l * b.q, m2 = b.l * b.p - b.f * b.q;
-    if (fabsf(m1) <= 1.0f && fabsf(m2) <= 1.0f) return true;
-    const float lo = fmax_std(slab_lo(m1, b.p + u * b.q), slab_lo(m2, u * b.p - b.q));
-    return fwd ? lo > 0.0f : lo < 0.0f;
+    const float b1 = b.p + u * b.q, b2 = u * b.p - b.q;
+    if (fwd) return fmin_std(slab_hi(m1, b1), slab_hi(m2, b2)) >= s0;
+    return fmax_std(slab_lo(m1, b1), slab_lo(m2, b2)) <= -s0;
 }
 
 MB_HD float box_z(const FoodBox &b, bool fwd)

@@ -516,28 +516,52 @@ static void world_phase_c(orc_sim *s, uint32_t wi)
 /* Sensor (Madrona RenderingSystem raycast; build-defined spec)*/
 /*                                                                           */
 /* 32 pinhole pixels per agent (24 forward over the 90-degree FOV, 8 backward,*/
-/* gfx.cpp:252-253) plus the forward centre "finder" ray.  Other agents are   */
-/* unit circles; in the agent's frame (f along the heading h, l along         */
-/* r = (hy, -hx)) the ray direction h + u r meets a circle iff                */
-/* q(u) = (A u - 2 l f) u + C <= 0 with A = f^2 - 1, C = l^2 - 1, and the hit */
-/* lies ahead of the ray iff f + u l > 0 (backward camera: < 0).  Live food   */
-/* packages are rotated +-1 squares (raster_box below).  Depth is view-space  */
-/* z: z = f - 1 for circles, the nearest corner's for squares (clamped at 0,  */
-/* 14-bit mantissa: zq), the ray's                                           */
-/* exit from the inner arena rectangle for the walls.  Each pixel takes the   */
-/* lexicographic minimum of (z, order): walls 0, food 1 + k, agents 64 + slot.*/
+/* gfx.cpp:252-253) plus the forward centre "finder" ray, cast horizontally   */
+/* from the agent's centre (attachEntityToView offset {0,0,0}, sim.cpp:221)   */
+/* and seeing only what lies beyond nearSphere = 1.1 from it (mgr.cpp:133):   */
+/* a ray hits an object iff it leaves the object at distance >= 1.1.  Other   */
+/* agents are circles of radius 0.92 (agent_render.obj's cross-section in the */
+/* rays' plane, z = 0 of the mesh: radii 0.910-0.921); food packages are the  */
+/* +-1 cube_render.obj boxes rotated about z (raster_box).  In the agent's    */
+/* frame (f along the heading h, l along r = (hy, -hx)) ray k runs along      */
+/* (1, u) forward / -(1, u) backward; its near point P0 = 1.1 (1, u)/|(1, u)| */
+/* (the ray parameter s0 = 1.1 / |(1, u)| along it).  Depth is view-space z   */
+/* (one per object): f - 0.92 for circles, the nearest corner's for squares   */
+/* (clamped at 0, 14-bit mantissa: zq); walls: the ray's exit from the inner  */
+/* arena rectangle when P0 lies in it, s0 when P0 lies inside a wall box, no  */
+/* wall (a miss: semantic -1, depth 255) when P0 lies beyond the walls.  Each */
+/* pixel takes the lexicographic minimum of (z, order): walls 0, food 1 + k,  */
+/* agents 64 + slot.                                                         */
 /* ------------------------------------------------------------------------ */
 static const float kInLo = 0.0f + 0.2f;     /* walls: makeWalls (sim.cpp:157-194), */
 static const float kInHiX = 128.0f - 0.2f;  /* 0.2-thick boxes on the boundary    */
 static const float kInHiY = 96.0f - 0.2f;
+static const float kOutLo = 0.0f - 0.2f;    /* the boxes' outer faces             */
+static const float kOutHiX = 128.0f + 0.2f;
+static const float kOutHiY = 96.0f + 0.2f;
+static const float kNearSphere = 1.1f;      /* mgr.cpp:133                        */
+static const float kAgentR = 0.92f;         /* agent disc radius in the ray plane */
+static const float kAgentR2 = 0.8464f;      /* kAgentR^2                          */
 
 /* pixel k's offset u = (2k + 1) / 24 - 1 (forward, k < 24) or
  * (2(k - 24) + 1) / 8 - 1 (backward), as one rounding: (2k - 23) * (1/24),
- * (2(k - 24) - 7) / 8 (exact) */
+ * (2(k - 24) - 7) / 8 (exact); the finder ray (k = 32) has u = 0 */
 static float ray_u(int k)
 {
     if (k < 24) return (float)(2 * k - 23) * (1.0f / 24.0f);
-    return (float)(2 * (k - 24) - 7) * 0.125f;
+    if (k < ORC_SENSOR) return (float)(2 * (k - 24) - 7) * 0.125f;
+    return 0.0f;
+}
+
+/* ray k's near point in the agent frame, (c, s) = 1.1 (1, u) / sqrt(1 + u^2)
+ * (c is also the ray parameter s0 of that point), and e = 1.1 sqrt(1 + u^2) */
+static void near_pt(int k, float *c, float *s, float *e)
+{
+    float u = ray_u(k);
+    float n = sqrtf(1.0f + u * u);
+    *c = kNearSphere / n;
+    *s = u * *c;
+    *e = kNearSphere * n;
 }
 
 /* ray direction k of heading (hx, hy) */
@@ -557,10 +581,25 @@ static void ray_dir(int k, float hx, float hy, float *dx, float *dy)
     }
 }
 
-/* wall depth: exit from the inner rectangle; 0 if the origin is in a wall box */
+static int in_inner(float x, float y)
+{
+    return x >= kInLo && x <= kInHiX && y >= kInLo && y <= kInHiY;
+}
+
+/* inside one of the four wall boxes (sim.cpp:168-180: centres (64, 0),
+ * (0, 48), (64, 96), (128, 48); half extents (64, 0.2), (0.2, 48), ...) */
+static int in_wall_box(float x, float y)
+{
+    int xs = x >= 0.0f && x <= 128.0f, ys = y >= 0.0f && y <= 96.0f;
+    int bx = (x >= kOutLo && x <= kInLo) || (x >= kInHiX && x <= kOutHiX);
+    int by = (y >= kOutLo && y <= kInLo) || (y >= kInHiY && y <= kOutHiY);
+    return (bx && ys) || (by && xs);
+}
+
+/* wall depth of a ray whose near point lies in the inner rectangle: its exit
+ * from the rectangle along (dx, dy) from the origin */
 static float wall_z(float ox, float oy, float dx, float dy)
 {
-    if (!(ox >= kInLo && ox <= kInHiX && oy >= kInLo && oy <= kInHiY)) return 0.0f;
     float tx = INFINITY, ty = INFINITY;
     if (dx > 0.0f) tx = (kInHiX - ox) / dx;
     else if (dx < 0.0f) tx = (kInLo - ox) / dx;
@@ -584,12 +623,11 @@ static inline float zq(float z)
     return z;
 }
 
-/* An object at view depth z hides the wall on ray (dx, dy) iff the ray meets
- * it strictly before leaving the inner rectangle, tested as z * d < (X - o)
- * per axis (no division); an origin inside a wall box sees the wall (z 0). */
+/* An object at view depth z hides the wall on ray (dx, dy) (near point in the
+ * inner rectangle) iff the ray meets it strictly before leaving the
+ * rectangle, tested as z * d < (X - o) per axis (no division). */
 static int beats_wall(float ox, float oy, float dx, float dy, float z)
 {
-    if (!(ox >= kInLo && ox <= kInHiX && oy >= kInLo && oy <= kInHiY)) return 0;
     if (dx > 0.0f) { if (!(z * dx < kInHiX - ox)) return 0; }
     else if (dx < 0.0f) { if (!(z * dx > kInLo - ox)) return 0; }
     if (dy > 0.0f) { if (!(z * dy < kInHiY - oy)) return 0; }
@@ -604,29 +642,31 @@ static inline void consider(orc_hit *h, float z, uint32_t order)
     if (z < h->z || (z == h->z && order < h->order)) { h->z = z; h->order = order; }
 }
 
-/* one object (unit circle at (cx, cy)) against all 33 rays of an agent */
+/* one object (a radius-0.92 circle at (cx, cy)) against all 33 rays of an
+ * agent.  Ray (1, u) meets the circle's line iff
+ * q(u) = (A u - 2 l f) u + C <= 0 (A = f^2 - R^2, C = l^2 - R^2); it leaves
+ * the circle beyond the near sphere iff its near point P0 lies inside the
+ * circle, or the chord's midpoint lies beyond P0: p >= e with p = f + u l
+ * (backward: -p).  Depth f - R (backward -f - R). */
 static void raster(orc_hit *hits, float ax, float ay, float hx, float hy, float cx, float cy,
                    uint32_t order)
 {
     float vx = cx - ax, vy = cy - ay;
     float f = vx * hx + vy * hy;
     float l = vx * hy - vy * hx;
-    float r2 = f * f + l * l;
-    if (r2 <= 1.0f) {
-        for (int k = 0; k <= ORC_SENSOR; ++k) consider(&hits[k], 0.0f, order);
-        return;
-    }
-    float A = f * f - 1.0f, B2 = 2.0f * (l * f), C = l * l - 1.0f;
-    float zf = zq(max0(f - 1.0f)), zb = zq(max0(-f - 1.0f));
-    for (int k = 0; k < ORC_SENSOR; ++k) {
-        float u = ray_u(k);
+    float A = f * f - kAgentR2, B2 = 2.0f * (l * f), C = l * l - kAgentR2;
+    float zf = zq(max0(f - kAgentR)), zb = zq(max0(-f - kAgentR));
+    for (int k = 0; k <= ORC_SENSOR; ++k) {
+        int fwd = k < 24 || k == ORC_SENSOR;
+        float u = ray_u(k), c, s, e;
+        near_pt(k, &c, &s, &e);
         float q = (A * u - B2) * u + C;
         float p = f + u * l;
-        if (!(q <= 0.0f)) continue;
-        if (k < 24) { if (p > 0.0f) consider(&hits[k], zf, order); }
-        else { if (p < 0.0f) consider(&hits[k], zb, order); }
+        float nx = fwd ? c - f : -c - f, ny = fwd ? s - l : -s - l;
+        int in0 = nx * nx + ny * ny <= kAgentR2;
+        int hit = in0 || (q <= 0.0f && (fwd ? p : -p) >= e);
+        if (hit) consider(&hits[k], fwd ? zf : zb, order);
     }
-    if (C <= 0.0f && f > 0.0f) consider(&hits[ORC_SENSOR], zf, order);
 }
 
 /* Food is the cube_render.obj +-1 box rotated about z by the package's draw
@@ -654,20 +694,19 @@ static void food_cs(uint32_t q22, float *c, float *s)
 /* In the agent frame (f along h, l along r) the square has centre (f, l) and
  * unit axes (p, q), (-q, p).  Ray u is the line Y = u X; with
  * S(v) = v.Y - u v.X the corners' S are S(centre) +- S(axis 1) +- S(axis 2),
- * so the line meets the square iff |l - u f| <= |q - u p| + |p + u q|.  The
- * square spans view depths f -+ (|p| + |q|): wholly ahead of the camera plane
- * it is hit by forward rays only (mirrored behind); straddling the plane, by
- * every ray when the origin is inside it (|m1|, |m2| <= 1: the origin in box
- * coordinates), else on the side of the chord, the sign of the slab entry
- * max_i lo_i.  Depth (one per object, like the circles' f - 1): the nearest
- * corner's view depth, max(0, f - (|p| + |q|)) forward, max(0, -(f + ...))
- * backward. */
+ * so the line meets the square iff |l - u f| <= |q - u p| + |p + u q|.  Along
+ * the ray s (1, u) the square's slabs give the parameter interval [lo, hi]
+ * (box coordinates s b_i - m_i, m1 = f p + l q, m2 = l p - f q, b1 = p + u q,
+ * b2 = u p - q); a forward ray leaves it beyond the near sphere iff
+ * hi >= s0, a backward one iff lo <= -s0 (s0 = 1.1 / |(1, u)|).  Depth (one
+ * per object, like the circles' f - R): the nearest corner's view depth,
+ * max(0, f - (|p| + |q|)) forward, max(0, -(f + ...)) backward. */
 static int box_line_hit(float f, float l, float p, float q, float u)
 {
     return fabsf(l - u * f) <= fabsf(q - u * p) + fabsf(p + u * q);
 }
 
-/* slab of one box axis along direction (1, u): lower end of t, or -inf */
+/* slab of one box axis along direction (1, u): lower / upper end of s */
 static float slab_lo(float m, float b)
 {
     if (b > 0.0f) return (m - 1.0f) / b;
@@ -675,15 +714,20 @@ static float slab_lo(float m, float b)
     return -INFINITY;
 }
 
-static int box_hit(float f, float l, float p, float q, float ext, float u, int fwd)
+static float slab_hi(float m, float b)
+{
+    if (b > 0.0f) return (m + 1.0f) / b;
+    if (b < 0.0f) return (m - 1.0f) / b;
+    return INFINITY;
+}
+
+static int box_hit(float f, float l, float p, float q, float u, int fwd, float s0)
 {
     if (!box_line_hit(f, l, p, q, u)) return 0;
-    if (f - ext > 0.0f) return fwd;
-    if (f + ext < 0.0f) return !fwd;
     float m1 = f * p + l * q, m2 = l * p - f * q;
-    if (fabsf(m1) <= 1.0f && fabsf(m2) <= 1.0f) return 1;
-    float lo = fmax_std(slab_lo(m1, p + u * q), slab_lo(m2, u * p - q));
-    return fwd ? lo > 0.0f : lo < 0.0f;
+    float b1 = p + u * q, b2 = u * p - q;
+    if (fwd) return fmin_std(slab_hi(m1, b1), slab_hi(m2, b2)) >= s0;
+    return fmax_std(slab_lo(m1, b1), slab_lo(m2, b2)) <= -s0;
 }
 
 static void raster_box(orc_hit *hits, float ax, float ay, float hx, float hy, float cx, float cy,
@@ -698,17 +742,44 @@ static void raster_box(orc_hit *hits, float ax, float ay, float hx, float hy, fl
     float q = c * hy - s * hx;
     float ext = fabsf(p) + fabsf(q);
     float zf = zq(max0(f - ext)), zb = zq(max0(-(f + ext)));
-    for (int k = 0; k < ORC_SENSOR; ++k) {
-        int fwd = k < 24;
-        if (box_hit(f, l, p, q, ext, ray_u(k), fwd)) consider(&hits[k], fwd ? zf : zb, order);
+    for (int k = 0; k <= ORC_SENSOR; ++k) {
+        int fwd = k < 24 || k == ORC_SENSOR;
+        float nc, ns, ne;
+        near_pt(k, &nc, &ns, &ne);
+        if (box_hit(f, l, p, q, ray_u(k), fwd, nc)) consider(&hits[k], fwd ? zf : zb, order);
     }
-    if (box_hit(f, l, p, q, ext, 0.0f, 1)) consider(&hits[ORC_SENSOR], zf, order);
 }
 
 static inline uint8_t depth_u8(float t)
 {
     if (!(t < 255.0f)) return 255;
     return (uint8_t)(int32_t)t;
+}
+
+/* what ray k of an agent at (ox, oy) with heading (hx, hy) sees, given its
+ * nearest object hit h (order 0xFFFFFFFF: none): h itself, the wall (order
+ * 0) or nothing (order ORC_MISS) */
+#define ORC_MISS 0xFFFFFFFEu
+static orc_hit resolve(orc_hit h, int k, float ox, float oy, float hx, float hy)
+{
+    int fwd = k < 24 || k == ORC_SENSOR;
+    float dx, dy, c, s, e;
+    ray_dir(k, hx, hy, &dx, &dy);
+    near_pt(k, &c, &s, &e);
+    float ex = c * hx + s * hy, ey = c * hy + s * (-hx);
+    float px = fwd ? ox + ex : ox - ex, py = fwd ? oy + ey : oy - ey;
+    int obj = h.order != 0xFFFFFFFFu;
+    orc_hit out = h;
+    if (in_inner(px, py)) {
+        if (!obj || !beats_wall(ox, oy, dx, dy, h.z)) { out.z = wall_z(ox, oy, dx, dy); out.order = 0; }
+    } else if (in_wall_box(px, py)) {
+        out.z = c;
+        out.order = 0;
+    } else if (!obj) {
+        out.z = INFINITY;
+        out.order = ORC_MISS;
+    }
+    return out;
 }
 
 static void world_phase_d(orc_sim *s, uint32_t wi)
@@ -739,23 +810,17 @@ static void world_phase_d(orc_sim *s, uint32_t wi)
             if (j == i) continue;
             raster(hits, a->x, a->y, hx, hy, w->ag[j].x, w->ag[j].y, 64u + (uint32_t)j);
         }
-        /* resolve each ray against the walls (order 0) */
-        for (int k = 0; k <= ORC_SENSOR; ++k) {
-            float dx, dy;
-            ray_dir(k, hx, hy, &dx, &dy);
-            if (hits[k].order == 0xFFFFFFFFu || !beats_wall(a->x, a->y, dx, dy, hits[k].z)) {
-                hits[k].z = wall_z(a->x, a->y, dx, dy);
-                hits[k].order = 0;
-            }
-        }
+        /* resolve each ray against the walls */
+        for (int k = 0; k <= ORC_SENSOR; ++k) hits[k] = resolve(hits[k], k, a->x, a->y, hx, hy);
         int8_t *sem = nc->sem + (size_t)a->obs_row * ORC_SENSOR;
         uint8_t *dep = nc->depth + (size_t)a->obs_row * ORC_SENSOR;
         for (int k = 0; k < ORC_SENSOR; ++k) {
             uint32_t o = hits[k].order;
-            sem[k] = (int8_t)(o == 0 ? 5 : (o < 64 ? 6 : w->ag[o - 64].species));
+            sem[k] = (int8_t)(o == ORC_MISS ? -1 : o == 0 ? 5 : (o < 64 ? 6 : w->ag[o - 64].species));
             dep[k] = depth_u8(hits[k].z);
         }
-        a->finder = hits[ORC_SENSOR].order >= 64 ? (int32_t)(hits[ORC_SENSOR].order - 64) : -1;
+        uint32_t fo = hits[ORC_SENSOR].order;
+        a->finder = (fo >= 64 && fo != ORC_MISS) ? (int32_t)(fo - 64) : -1;
     }
 }
 
@@ -959,6 +1024,27 @@ int32_t orc_world_food(const orc_sim *s, uint32_t wi, int32_t *out)
             ++k;
         }
     return k;
+}
+
+void orc_probe_agent(float ax, float ay, float hx, float hy, float cx, float cy, uint8_t *hit, float *z)
+{
+    orc_hit hits[ORC_SENSOR + 1];
+    for (int k = 0; k <= ORC_SENSOR; ++k) { hits[k].z = INFINITY; hits[k].order = 0xFFFFFFFFu; }
+    raster(hits, ax, ay, hx, hy, cx, cy, 64u);
+    for (int k = 0; k <= ORC_SENSOR; ++k) {
+        hit[k] = hits[k].order == 64u;
+        z[k] = hits[k].z;
+    }
+}
+
+void orc_probe_walls(float ax, float ay, float hx, float hy, int8_t *sem, uint8_t *depth)
+{
+    for (int k = 0; k <= ORC_SENSOR; ++k) {
+        orc_hit none = {INFINITY, 0xFFFFFFFFu};
+        orc_hit h = resolve(none, k, ax, ay, hx, hy);
+        sem[k] = (int8_t)(h.order == ORC_MISS ? -1 : 5);
+        depth[k] = depth_u8(h.z);
+    }
 }
 
 void orc_probe_box(float ax, float ay, float hx, float hy, float cx, float cy, uint32_t rot,

@@ -93,6 +93,12 @@ int32_t  orc_world_food(const orc_sim *s, uint32_t w, int32_t *out);
  * the finder ray last) */
 void     orc_probe_box(float ax, float ay, float hx, float hy, float cx, float cy,
                        uint32_t rot, uint8_t *hit, float *z);
+/* the same for another agent's disc centred at (cx, cy) */
+void     orc_probe_agent(float ax, float ay, float hx, float hy, float cx, float cy,
+                         uint8_t *hit, float *z);
+/* what each ray of a lone agent sees of the walls: sem[k] (5 wall, -1 miss)
+ * and depth[k] bytes (the finder ray last: 5 / -1) */
+void     orc_probe_walls(float ax, float ay, float hx, float hy, int8_t *sem, uint8_t *depth);
 void     orc_threefry2x32(const uint32_t key[2], const uint32_t ctr[2],
                           uint32_t out[2]);
 float    orc_sample_uniform(uint32_t bits);

@@ -82,6 +82,8 @@ def lib():
         L.orc_sample_i32.argtypes = [u32, i32, i32]
         f32 = ctypes.c_float
         L.orc_probe_box.argtypes = [f32, f32, f32, f32, f32, f32, u32, vp, vp]
+        L.orc_probe_agent.argtypes = [f32, f32, f32, f32, f32, f32, vp, vp]
+        L.orc_probe_walls.argtypes = [f32, f32, f32, f32, vp, vp]
         L.orc_action_hash.restype = u32
         L.orc_action_hash.argtypes = [u32, u32, u32, u32]
         _LIB = L
@@ -104,6 +106,25 @@ def probe_box(agent, heading, centre, rot):
                         float(centre[0]), float(centre[1]), int(rot), hit.ctypes.data,
                         z.ctypes.data)
     return hit.astype(bool), z
+
+
+def probe_agent(agent, heading, centre):
+    """Rays of one agent against another agent's disc: (hit[33] bool, z[33] f32)."""
+    hit = np.zeros(33, np.uint8)
+    z = np.zeros(33, np.float32)
+    lib().orc_probe_agent(float(agent[0]), float(agent[1]), float(heading[0]), float(heading[1]),
+                          float(centre[0]), float(centre[1]), hit.ctypes.data, z.ctypes.data)
+    return hit.astype(bool), z
+
+
+def probe_walls(agent, heading):
+    """Rays of a lone agent against the walls: (sem[33] int8: 5 wall / -1 miss,
+    depth[33] uint8), the finder ray last."""
+    sem = np.zeros(33, np.int8)
+    dep = np.zeros(33, np.uint8)
+    lib().orc_probe_walls(float(agent[0]), float(agent[1]), float(heading[0]), float(heading[1]),
+                          sem.ctypes.data, dep.ctypes.data)
+    return sem, dep
 
 
 class OracleSim:

@@ -7,8 +7,9 @@
        loaded with torch.load(weights_only=True)): observation width 69 and
        action width 6 (learn/env.py:19, learn/util.py:23-28);
      * mesh extents (data/agent_render.obj, data/cube_render.obj, read as text)
-       behind the sensor objects (agents: unit circles; food: the +-1 cube as a
-     rotated square).
+       behind the sensor objects, and the agent mesh's cross-section in the
+       rays' plane (agents: discs of radius 0.92; food: the +-1 cube as a
+       rotated square).
 2. oracle_w4_a32_s69.npz / oracle_w8_a4_s7_fixed.npz -- golden vectors of the
    CPU oracle (oracle/mbots_oracle.c, the parity checker): per-step SHA-256
    digests of every exported column after step() and after
@@ -90,6 +91,33 @@ def obj_extent(path):
     return float(np.abs(xs).max())
 
 
+def obj_section_radii(path, z=0.0):
+    """Radii (min, max) of the mesh's cross-section with the plane Z = z: the
+    outline horizontal sensor rays at the camera's height meet (cameras sit at
+    the agent's centre, sim.cpp:220-221; every agent and food entity stands at
+    z = 1 with scale 1, sim.cpp:204-211, :332-345)."""
+    V, F = [], []
+    with open(path) as f:
+        for line in f:
+            t = line.split()
+            if not t:
+                continue
+            if t[0] == "v":
+                V.append([float(v) for v in t[1:4]])
+            elif t[0] == "f":
+                F.append([int(x.split("/")[0]) - 1 for x in t[1:]])
+    V = np.array(V)
+    pts = []
+    for face in F:
+        for i in range(len(face)):
+            a, b = V[face[i]], V[face[(i + 1) % len(face)]]
+            if (a[2] - z) * (b[2] - z) < 0 or (a[2] == z) != (b[2] == z):
+                t = (z - a[2]) / (b[2] - a[2])
+                pts.append(a + (b - a) * t)
+    r = np.linalg.norm(np.array(pts)[:, :2], axis=1)
+    return [round(float(r.min()), 6), round(float(r.max()), 6)]
+
+
 def reference_shapes():
     import torch
     out = {"source": "read from /root/reference by tests/golden/make_golden.py"}
@@ -109,6 +137,8 @@ def reference_shapes():
     out["action_dim"] = sorted({v["action_dim"] for v in species.values()})
     out["mesh_abs_extent"] = {m: obj_extent(f"{REF}/data/{m}")
                              for m in ("agent_render.obj", "cube_render.obj")}
+    # the agent disc of the sensor spec: radius 0.92 covers this
+    out["agent_section_z0_radii"] = obj_section_radii(f"{REF}/data/agent_render.obj")
     return out
 
 

@@ -34,9 +34,14 @@ def test_reference_boundary_shapes():
     assert widths[po.COL_DEPTH] + widths[po.COL_HEALTH] + widths[po.COL_POS] + \
         widths[po.COL_SEMANTIC] + widths[po.COL_SURROUND] == ref["obs_dim"][0]
     assert widths[po.COL_ACTION] == ref["action_dim"][0]
-    # sensor objects: agents ~ the unit icosphere (extent 1.12), food the +-1 cube
+    # sensor objects: food the +-1 cube; agents the agent mesh's cross-section
+    # in the rays' plane (z = 0 of the mesh: the camera sits at the agent's
+    # centre), radii 0.910-0.921 -> the spec's disc of radius 0.92, which the
+    # near sphere 1.1 (mgr.cpp:133) clears, so a camera never sees its own body
     ext = ref["mesh_abs_extent"]
     assert 1.0 <= ext["agent_render.obj"] <= 1.2 and ext["cube_render.obj"] == 1.0
+    lo, hi = ref["agent_section_z0_radii"]
+    assert lo <= 0.92 and abs(hi - 0.92) < 1e-3 and hi < 1.1
 
 
 def test_golden_final_tables_consistent():

@@ -194,7 +194,7 @@ def test_export_invariants_and_shift():
         assert list(np.bincount(sp, minlength=5)[1:]) == list(sc.sum(0))
         assert (sim.column(po.COL_HEALTH) > 0).all()
         sem = sim.column(po.COL_SEMANTIC)
-        assert sem.min() >= 1 and sem.max() <= 6
+        assert set(np.unique(sem).tolist()) <= {-1, 1, 2, 3, 4, 5, 6}   # -1: a miss
         sim.shift_observations()
         for c in (po.COL_SPECIES, po.COL_POS, po.COL_HEALTH, po.COL_SURROUND, po.COL_REWARD,
                   po.COL_ACTION, po.COL_HIDDEN):
@@ -262,9 +262,147 @@ def test_food_box_behind_uses_backward_camera():
     assert abs(float(z[27]) - (10.0 - 2.0 ** 0.5)) < 1e-3
 
 
-def test_food_box_containing_the_agent_fills_every_ray():
-    hit, z = po.probe_box((20.3, 20.2), (0.6, 0.8), (20.0, 20.0), 12345)
-    assert hit.all() and (z == 0.0).all()
+def test_food_box_containing_the_agent_near_sphere():
+    # the agent at the centre of an axis-aligned box, heading +x: ray (1, u)
+    # leaves the box at X = 1, t = sqrt(1 + u^2), seen iff t >= 1.1 (nearSphere,
+    # mgr.cpp:133): |u| >= 0.458 -> forward pixels 0..6, 17..23, backward
+    # u = +-7/8, +-5/8 (24, 25, 30, 31); the finder (t = 1) sees nothing of it
+    hit, z = po.probe_box((20.0, 20.0), (1.0, 0.0), (20.0, 20.0), 0)
+    assert _hit_pixels(hit) == list(range(7)) + list(range(17, 26)) + [30, 31]
+    assert (z[hit] == 0.0).all()
+
+
+# ---- the near sphere and the agent disc -------------------
+R_AGENT, NEAR = 0.92, 1.1
+
+
+def _dirs(heading):
+    """World directions of the 33 rays (float64): 24 forward, 8 backward, finder."""
+    hx, hy = heading
+    out = []
+    for k in range(33):
+        u = (2 * k - 23) / 24 if k < 24 else ((2 * (k - 24) - 7) / 8 if k < 32 else 0.0)
+        sg = -1.0 if 24 <= k < 32 else 1.0
+        out.append((sg * (hx + u * hy), sg * (hy - u * hx)))
+    return np.array(out)
+
+
+def _ref_disc(agent, heading, centre, R=R_AGENT):
+    """Independent float64 restatement: ray k sees the disc iff it leaves it at
+    distance >= 1.1; returns (hit[33], margin[33]) -- margin: how far the ray
+    is from either decision boundary (tangency, t_exit = 1.1)."""
+    d = _dirs(heading)
+    d /= np.linalg.norm(d, axis=1)[:, None]
+    v = np.array(centre, np.float64) - np.array(agent, np.float64)
+    tm = d @ v
+    dist2 = v @ v - tm * tm
+    half = np.sqrt(np.maximum(R * R - dist2, 0.0))
+    hit = (dist2 <= R * R) & (tm + half >= NEAR)
+    margin = np.minimum(np.abs(R * R - dist2), np.where(dist2 <= R * R, np.abs(tm + half - NEAR), 1.0))
+    return hit, margin
+
+
+def _ref_box(agent, heading, centre, rot22):
+    """float64 slab restatement for a food square (rotation = quarter-turn
+    fraction * pi/2): hit iff the ray's parameter interval in the square is
+    non-empty and it exits at distance >= 1.1."""
+    w = rot22 * (np.pi / 2) / 4194304.0
+    a1 = np.array([np.cos(w), np.sin(w)])
+    a2 = np.array([-np.sin(w), np.cos(w)])
+    d = _dirs(heading)
+    d /= np.linalg.norm(d, axis=1)[:, None]
+    o = np.array(agent, np.float64) - np.array(centre, np.float64)
+    lo = np.full(33, -np.inf)
+    hi = np.full(33, np.inf)
+    for ax in (a1, a2):
+        b = d @ ax
+        m = o @ ax
+        with np.errstate(divide="ignore", invalid="ignore"):
+            t1, t2 = (-1.0 - m) / b, (1.0 - m) / b
+        lo = np.maximum(lo, np.where(b != 0, np.minimum(t1, t2), np.where(abs(m) <= 1, -np.inf, np.inf)))
+        hi = np.minimum(hi, np.where(b != 0, np.maximum(t1, t2), np.where(abs(m) <= 1, np.inf, -np.inf)))
+    hit = (lo <= hi) & (hi >= NEAR)
+    margin = np.minimum(np.abs(hi - lo), np.abs(hi - NEAR))
+    return hit, margin
+
+
+def test_disc_at_1_5_ahead():
+    # centre 1.5 ahead: the line reaches the 0.92 disc for |u| <= 0.777 (pixels
+    # 3..20) and every such ray leaves it beyond 1.1; depth f - R = 0.58
+    hit, z = po.probe_agent((30.0, 30.0), (1.0, 0.0), (31.5, 30.0))
+    assert _hit_pixels(hit) == list(range(3, 21)) + [32]
+    assert (np.abs(z[hit] - 0.58) < 1e-3).all()
+    ref, _ = _ref_disc((30.0, 30.0), (1.0, 0.0), (31.5, 30.0))
+    assert np.array_equal(hit, ref)
+
+
+def test_disc_at_0_9_ahead_overlapping_bodies():
+    # centre 0.9 ahead: the camera lies inside the other agent's disc; rays see
+    # its far side where it reaches past the near sphere (the finder does:
+    # its near point (1.1, 0) is 0.2 from the centre); depth clamps at 0
+    hit, z = po.probe_agent((30.0, 30.0), (1.0, 0.0), (30.9, 30.0))
+    ref, margin = _ref_disc((30.0, 30.0), (1.0, 0.0), (30.9, 30.0))
+    assert margin.min() > 1e-4
+    assert np.array_equal(hit, ref)
+    assert hit[32] and hit[:24].any() and not hit[24:32].any()
+    assert (z[hit] == 0.0).all()
+
+
+def test_disc_inside_the_near_sphere_is_invisible():
+    # 0.1 + 0.92 < 1.1: the whole disc lies inside the near sphere
+    for c in ((30.1, 30.0), (30.0, 30.05), (29.9, 30.0)):
+        hit, _ = po.probe_agent((30.0, 30.0), (1.0, 0.0), c)
+        assert not hit.any(), c
+
+
+def test_disc_behind_is_seen_by_backward_pixels():
+    hit, z = po.probe_agent((30.0, 30.0), (0.0, 1.0), (30.0, 28.5))
+    ref, _ = _ref_disc((30.0, 30.0), (0.0, 1.0), (30.0, 28.5))
+    assert np.array_equal(hit, ref)
+    assert _hit_pixels(hit) == list(range(25, 31))      # |u| <= 0.777: not +-7/8
+    assert (np.abs(z[hit] - 0.58) < 1e-3).all()
+
+
+def test_disc_and_box_predicates_match_float64_restatement():
+    """2000 random (agent, heading, object) configurations within 4 units:
+    every ray not within 1e-4 of a decision boundary agrees with the float64
+    geometry (discs of radius 0.92, rotated unit squares, near sphere 1.1)."""
+    rng = np.random.default_rng(7)
+    checked = 0
+    for t in range(2000):
+        a = rng.uniform(10, 60, 2).astype(np.float32)
+        th = rng.uniform(0, 2 * np.pi)
+        h = (np.float32(np.cos(th)), np.float32(np.sin(th)))
+        c = (a + rng.uniform(-4, 4, 2)).astype(np.float32)
+        if t % 2:
+            hit, _ = po.probe_agent(a, h, c)
+            ref, margin = _ref_disc(a.astype(np.float64), np.array(h, np.float64), c.astype(np.float64))
+        else:
+            rot = int(rng.integers(0, 1 << 22))
+            hit, _ = po.probe_box(a, h, c, rot)
+            ref, margin = _ref_box(a.astype(np.float64), np.array(h, np.float64), c.astype(np.float64), rot)
+        ok = margin > 1e-4
+        assert np.array_equal(hit[ok], ref[ok]), (t, a, h, c)
+        checked += int(ok.sum())
+    assert checked > 60000
+
+
+def test_walls_near_sphere_classes():
+    # agent 0.5 from the left wall looking at it: every forward near point lies
+    # beyond the wall box (x < -0.2): a miss (semantic -1, depth 255); the
+    # backward pixels see the right wall's inner face 127.3 away
+    sem, dep = po.probe_walls((0.5, 50.0), (-1.0, 0.0))
+    assert (sem[:24] == -1).all() and sem[32] == -1 and (dep[:24] == 255).all()
+    assert (sem[24:32] == 5).all() and dep[27] == dep[28] == 127
+    # 1.0 from it: the central near points fall inside the wall box (the wall,
+    # depth s0 = 1.1 / |(1, u)| -> byte 1), the outer ones still in the arena
+    # (the wall's face 0.8 ahead along the heading -> byte 0)
+    sem, dep = po.probe_walls((1.0, 50.0), (-1.0, 0.0))
+    assert (sem[:24] == 5).all() and sem[32] == 5
+    assert dep[11] == dep[12] == dep[32] == 1 and dep[0] == dep[23] == 0
+    # the arena's middle: every ray ends on a wall
+    sem, dep = po.probe_walls((64.0, 48.0), (1.0, 0.0))
+    assert (sem == 5).all() and dep[11] == 63 and dep[27] == 63
 
 
 def test_food_box_rotation_follows_heading_frame():
