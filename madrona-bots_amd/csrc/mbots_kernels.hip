@@ -1032,7 +1032,7 @@ __device__ __forceinline__ void run_survivors(LDS &L, int nf, int a0, int q0, in
             // side of the camera plane (circle: |f| > 2.05 > 1.1 + 0.92; square:
             // |f| > 2.6 > 1.1 + its half-diagonal 1.42, so every corner has
             // |X| >= 1.18).  Its hit interval in u, approximately: the circle's
-            // roots (lf -+ sqrt(r^2 - R^2)) / (f^2 - R^2), or the square's
+            // roots (lf -+ R sqrt(r^2 - R^2)) / (f^2 - R^2), or the square's
             // extreme corner slopes Y / X.
             const bool fwd = f > 0.0f;
             const float sc = fwd ? 12.0f : 4.0f;
@@ -1049,7 +1049,7 @@ __device__ __forceinline__ void run_survivors(LDS &L, int nf, int a0, int q0, in
                 ulo = fminf(fminf(s0, s1), fminf(s2, s3));
                 uhi = fmaxf(fmaxf(s0, s1), fmaxf(s2, s3));
             } else {
-                const float sq = __builtin_amdgcn_sqrtf(r2 - kAgentR2);
+                const float sq = __builtin_amdgcn_sqrtf(kAgentR2 * (r2 - kAgentR2));
                 const float ia = __builtin_amdgcn_rcpf(f * f - kAgentR2);
                 const float lf = l * f;
                 ulo = (lf - sq) * ia;
