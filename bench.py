@@ -27,6 +27,7 @@ actions and memory written back) at 4096 worlds/GPU -- BASELINE config 2,
 own HBM roofline.
 """
 import argparse
+import datetime
 import json
 import os
 import sys
@@ -184,8 +185,11 @@ def reference_loop(W, args, rank, world_size, dev, distributed, label):
         m.hidden_state_tensor(False).to_torch()
         rew = m.reward_tensor(False).to_torch().clone()      # :49-50
         hp = m.health_tensor(False).to_torch().clone()
-        obs = m.construct_obs(False)                         # util.construct_obs, every species
-        prev = m.construct_obs(True)                         # :86
+        # util.construct_obs of the previous rows (:86) issued before the current
+        # rows' (:58-70): it needs no sensor rows, so it runs beside the sensor
+        # instead of queueing behind the current rows' wait for it
+        prev = m.construct_obs(True)
+        obs = m.construct_obs(False)                         # every species at once
         ph = m.hidden_state_tensor(True).to_torch()          # :88
         m.shift_observations()                               # :135
         m.write_synthetic_actions(ACTION_SEED, t + 1, True)  # :136-137 actions + memory
@@ -385,9 +389,11 @@ def main():
         torch.cuda.set_stream(torch.cuda.Stream(device=dev, priority=-1))
     if distributed:
         if args.backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
+            # (a bounded timeout: a collective that cannot complete ends the run
+            # with an error instead of holding the node)
+            dist.init_process_group("nccl", device_id=dev, timeout=datetime.timedelta(seconds=300))
         else:
-            dist.init_process_group(args.backend)
+            dist.init_process_group(args.backend, timeout=datetime.timedelta(seconds=300))
 
     import madrona_bots as mb
     W = args.worlds
@@ -453,7 +459,10 @@ def main():
     # bench runs several ranks (so the driver's 1..8-GPU run covers it)
     cfg5 = None
     if distributed or args.gather:
-        cfg5 = config5_loop(mgr, args, rank, world_size, dev, distributed)
+        try:
+            cfg5 = config5_loop(mgr, args, rank, world_size, dev, distributed)
+        except Exception as e:   # reported in the line; the main measurement stands
+            cfg5 = {"error": f"{type(e).__name__}: {e}"[:400]}
     secondary = ref_main = None
     if not args.no_secondary:
         secondary = reference_loop(4096, args, rank, world_size, dev, distributed,

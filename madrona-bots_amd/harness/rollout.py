@@ -60,8 +60,11 @@ def random_rollout(sim, steps, seed=1234, shift_per_species=False, device=None, 
         action = sim.action_tensor(False).to_torch()
         new_actions = []
         if fused:
-            obs_all = sim.construct_obs(False)
+            # the previous rows first: they need no sensor rows, so their
+            # kernel runs beside the sensor instead of queueing behind the
+            # current rows' wait for it (the two reads are independent)
             prev_all = sim.construct_obs(True) if t > 0 else None
+            obs_all = sim.construct_obs(False)
         for sp, (s, e) in enumerate(offsets):
             if fused and not (shift_per_species and sp > 0):
                 obs = obs_all[s:e]

@@ -78,7 +78,11 @@ def _load():
         "mbots_kernel_times": [vp, P(ctypes.c_double), P(ctypes.c_uint64)],
     }
     for name, args in sig.items():
-        fn = getattr(L, name)
+        # (a symbol an older build lacks -- A/B runs through MBOTS_LIB -- stays
+        # absent: calling it raises AttributeError)
+        fn = getattr(L, name, None)
+        if fn is None and os.environ.get("MBOTS_LIB"):
+            continue
         fn.argtypes = args
         fn.restype = ctypes.c_int
     L.mbots_last_error.restype = ctypes.c_char_p
