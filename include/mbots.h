@@ -39,8 +39,10 @@ extern "C" {
  * shard's last world reads the same SpeciesInfo row as on one device
  * (sim.cpp:943).  The ghost's agents act on what
  * mbots_write_synthetic_actions writes (the identity-keyed stream is keyed by
- * global world, so with it N shards == one device exactly).  Every shard but
- * the last sets it. */
+ * global world, so with it N shards == one device exactly); its rows lie past
+ * row N, outside every exported view, so a learner writing actions through
+ * the views leaves them to replay their last actions (carried through the row
+ * moves and the shift like every row's).  Every shard but the last sets it. */
 #define MBOTS_FLAG_SHARD_GHOST      0x4u
 
 /* execution modes (madrona::ExecMode; the reference's callers pick CPU when

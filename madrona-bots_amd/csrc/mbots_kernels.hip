@@ -926,12 +926,14 @@ constexpr float kWedge = 1.41421356f * kAgentR + 0.05f;
 constexpr float kUEps = 2e-3f;                // root-interval margin in u
 // food squares lie inside their circumscribed circle, radius sqrt 2 (1.42 with
 // margin): the wedge |l| <= |f| + sqrt(2) 1.42; candidate pixels from the
-// corner slopes when |f| > kFoodFar (the square then lies wholly beyond the
-// near sphere, on one side of the camera plane), every ray exactly (the wide
-// list) otherwise; discs likewise beyond kCircleFar (> 1.1 + 0.92)
+// corner slopes when |f| > kFoodFar and r^2 > kFoodFar2 (the square then lies
+// wholly beyond the near sphere, on one side of the camera plane), every ray
+// exactly (the wide list) otherwise; discs likewise when |f| > 1.5 and
+// r^2 > kCircleFar2
 constexpr float kWedgeFood = 1.41421356f * 1.42f + 0.05f;
-constexpr float kFoodFar = 2.6f;
-constexpr float kCircleFar = 2.05f;
+constexpr float kFoodFar = 2.5f;
+constexpr float kFoodFar2 = 6.5f;       // (1.1 + 1.4142)^2 = 6.32: a square wholly beyond the near sphere
+constexpr float kCircleFar2 = 4.2f;     // (1.1 + 0.92)^2 = 4.08: a disc wholly beyond it
 constexpr float kFarCull = 5.0f;               // P1 angular cull from this |f| on
 
 template <int kCap>
@@ -948,7 +950,16 @@ struct SensorLDS {
                                               // sink slot for the branch-free write); a
                                               // survivor batch's wide pairs are compacted
                                               // into its own range
-    alignas(16) float u[kSensor];
+};
+
+// per ray k (32 pixels, the finder at 32): offset u and near point NearPt
+// {c, s, e} (near_pt), one table per block (every wave writes
+// the same bits before reading it: no barrier needed)
+struct RayTab {
+    alignas(16) float u[36];
+    alignas(16) float c[36];
+    alignas(16) float s[36];
+    alignas(16) float e[36];
 };
 
 // pinhole offsets u = (2k + 1) / 24 - 1 forward, (2k' + 1) / 8 - 1 backward,
@@ -977,13 +988,13 @@ __device__ __forceinline__ void pair_fl(const LDS &L, int nf, int i, int j, floa
 // W: wide pairs qcode[q0, q0 + cnt), two per wave (32 lanes each: rays 0..31,
 // lane 0 of each half also takes the finder ray)
 template <class LDS>
-__device__ __forceinline__ void run_wide(LDS &L, int nf, int a0, int q0, int cnt)
+__device__ __forceinline__ void run_wide(LDS &L, const RayTab &R, int nf, int a0, int q0, int cnt)
 {
     const int lane = (int)__lane_id();
     // ray k's offset and near point (the near sphere): loop invariant
     const int k = lane & 31;
-    const float uk = L.u[k];
-    const NearPt np = near_pt(uk), fnp = finder_np();
+    const float uk = R.u[k];
+    const NearPt np{R.c[k], R.s[k], R.e[k]}, fnp{R.c[kSensor], R.s[kSensor], R.e[kSensor]};
     for (int e0 = 0; e0 < cnt; e0 += 2) {
         const int e = e0 + (lane >> 5);
         if (e < cnt) {
@@ -1012,7 +1023,7 @@ __device__ __forceinline__ void run_wide(LDS &L, int nf, int a0, int q0, int cnt
 // candidate pixels; the edge pixels and the finder get the exact test inline,
 // near pairs go to the wide list
 template <class LDS>
-__device__ __forceinline__ void run_survivors(LDS &L, int nf, int a0, int q0, int cnt)
+__device__ __forceinline__ void run_survivors(LDS &L, const RayTab &R, int nf, int a0, int q0, int cnt)
 {
     const int lane = (int)__lane_id();
     bool wide = false;
@@ -1025,13 +1036,14 @@ __device__ __forceinline__ void run_survivors(LDS &L, int nf, int a0, int q0, in
         pair_fl(L, nf, a0 + ic, j, f, l, order);
         const bool food = j < nf;
         const float r2 = f * f + l * l;
-        if (fabsf(f) <= (food ? kFoodFar : kCircleFar)) {
+        if ((fabsf(f) <= (food ? kFoodFar : 1.5f)) | (r2 <= (food ? kFoodFar2 : kCircleFar2))) {
             wide = true;
         } else {
-            // A far pair: the object lies wholly beyond the near sphere, on one
-            // side of the camera plane (circle: |f| > 2.05 > 1.1 + 0.92; square:
-            // |f| > 2.6 > 1.1 + its half-diagonal 1.42, so every corner has
-            // |X| >= 1.18).  Its hit interval in u, approximately: the circle's
+            // A far pair: the object lies wholly beyond the near sphere
+            // (circle: r > 2.02 = 1.1 + 0.92; square: r > 2.55 > 1.1 + its
+            // half-diagonal 1.4142) and on one side of the camera plane
+            // (circle: |f| > 1.5; square: |f| > 2.5, so every corner has
+            // |X| >= 1.08).  Its hit interval in u, approximately: the circle's
             // roots (lf -+ R sqrt(r^2 - R^2)) / (f^2 - R^2), or the square's
             // extreme corner slopes Y / X.
             const bool fwd = f > 0.0f;
@@ -1070,11 +1082,11 @@ __device__ __forceinline__ void run_survivors(LDS &L, int nf, int a0, int q0, in
             // u) inside the true interval, where the approximate bounds are off
             // by ~1e-6: for a circle the float q(u) is then off by < 1e-4 of a
             // value <= -0.08; for a square every corner's S = Y - u X is
-            // >= 1.18 x 0.08 from 0 (|X| >= 1.18), against a float error of the
+            // >= 1.08 x 0.08 from 0 (|X| >= 1.08), against a float error of the
             // line test < 1e-4.  They are hits carrying the object's key (a far
             // object lies beyond the near sphere: nothing of it is clipped).
             const int kl = k0 + max(c - 1, 0);
-            const float ua = L.u[k0 & 31], ub = L.u[kl & 31];
+            const float ua = R.u[k0 & 31], ub = R.u[kl & 31];
             bool ha, hb, hf;
             uint32_t kin;
             if (food) {   // a far square: box_hit is the line test on its side
@@ -1101,7 +1113,7 @@ __device__ __forceinline__ void run_survivors(LDS &L, int nf, int a0, int q0, in
     const int nw = __popcll(wm);
     if (nw > 0) {
         wave_sync();
-        run_wide(L, nf, a0, q0, nw);
+        run_wide(L, R, nf, a0, q0, nw);
         wave_sync();
     }
 }
@@ -1164,6 +1176,7 @@ __global__ __launch_bounds__(64 * kSensorWorlds, kCap <= 128 ? MB_SENSOR_BLOCKS 
 {
     constexpr int kG = kCap / 64;   // 64-slot groups
     __shared__ SensorLDS<kCap> lds[kSensorWorlds];
+    __shared__ RayTab R;
     const uint32_t wv = threadIdx.x >> 6;
     const uint32_t lane = threadIdx.x & 63u;
     static_assert(kSensorWorlds % kSplit == 0, "split must divide the block's waves");
@@ -1173,7 +1186,14 @@ __global__ __launch_bounds__(64 * kSensorWorlds, kCap <= 128 ? MB_SENSOR_BLOCKS 
     if (w >= S.W) return;
     SensorLDS<kCap> &L = lds[wv];
     constexpr bool depth = kDepth;
-    if (lane < kSensor) L.u[lane] = u_of((int)lane);
+    if (lane <= kSensor) {   // ray `lane` (the finder at u = 0: near_pt(0) = {1.1, 0, 1.1})
+        const float u = lane < kSensor ? u_of((int)lane) : 0.0f;
+        const NearPt np = near_pt(u);
+        R.u[lane] = u;
+        R.c[lane] = np.c;
+        R.s[lane] = np.s;
+        R.e[lane] = np.e;
+    }
     SensorPrefetch pf;
     sensor_prefetch(S, w, lane, pf);
     {
@@ -1286,14 +1306,14 @@ __global__ __launch_bounds__(64 * kSensorWorlds, kCap <= 128 ? MB_SENSOR_BLOCKS 
                 nq += __popcll(m);
                 if (nq >= 64) {
                     wave_sync();
-                    run_survivors(L, nf, a0, nq - 64, 64);
+                    run_survivors(L, R, nf, a0, nq - 64, 64);
                     nq -= 64;
                 }
             }
         }
         if (nq > 0) {
             wave_sync();
-            run_survivors(L, nf, a0, 0, nq);
+            run_survivors(L, R, nf, a0, 0, nq);
         }
         wave_sync();
         // ---- output: keys vs walls; lane = (agent ci, pixels 4g .. 4g+3) ----
@@ -1303,7 +1323,7 @@ __global__ __launch_bounds__(64 * kSensorWorlds, kCap <= 128 ? MB_SENSOR_BLOCKS 
             const int i = a0 + cc;
             const float2 p = L.obj[nf + i], h = L.hd[i];
             const uint4 kv4 = *reinterpret_cast<const uint4 *>(&L.key[cc * kKeyStride + 4 * g]);
-            const float4 u4 = *reinterpret_cast<const float4 *>(&L.u[4 * g]);
+            const float4 u4 = *reinterpret_cast<const float4 *>(&R.u[4 * g]);
             // the chunk's 64-slot group (8 | 64: one group per chunk), a uniform branch
             int r;
             if constexpr (kG == 2) {
@@ -1337,10 +1357,12 @@ __global__ __launch_bounds__(64 * kSensorWorlds, kCap <= 128 ? MB_SENSOR_BLOCKS 
                 int cls = kWallInner;
                 float s0 = 0.0f;
                 if (!deep) {
-                    const NearPt np = near_pt(u);
-                    const float ex = np.c * h.x + np.s * h.y, ey = np.c * h.y + np.s * (-h.x);
-                    cls = wall_class(fw ? p.x + ex : p.x - ex, fw ? p.y + ey : p.y - ey);
-                    s0 = np.c;
+                    const int k = 4 * g + t;
+                    const float c = R.c[k], sn = R.s[k];
+                    const float ex = c * h.x + sn * h.y, ey = c * h.y + sn * (-h.x);
+                    const float px = fw ? p.x + ex : p.x - ex, py = fw ? p.y + ey : p.y - ey;
+                    if (!inside_arena(px, py)) cls = in_wall_box(px, py) ? kWallBox : kWallNone;
+                    s0 = c;
                 }
                 const bool obj = (kv != kNoKey) &
                                  (cls == kWallInner ? beats_wall(p.x, p.y, dx, dy, oz) : cls == kWallNone);
@@ -1366,9 +1388,14 @@ __global__ __launch_bounds__(64 * kSensorWorlds, kCap <= 128 ? MB_SENSOR_BLOCKS 
             const float2 p = L.obj[nf + i], h = L.hd[i];
             const uint32_t kv = L.key[lane * kKeyStride + kSensor];
             const uint32_t order = kv & kOrderMask;
-            const NearPt fnp = finder_np();
-            const float ex = fnp.c * h.x + fnp.s * h.y, ey = fnp.c * h.y + fnp.s * (-h.x);
-            const int cls = wall_class(p.x + ex, p.y + ey);
+            const bool deep = (p.x >= kInLo + 1.2f) & (p.x <= kInHiX - 1.2f) & (p.y >= kInLo + 1.2f) &
+                              (p.y <= kInHiY - 1.2f);
+            int cls = kWallInner;
+            if (!deep) {
+                const float c = R.c[kSensor], sn = R.s[kSensor];
+                const float ex = c * h.x + sn * h.y, ey = c * h.y + sn * (-h.x);
+                cls = wall_class(p.x + ex, p.y + ey);
+            }
             const bool agent = (kv != kNoKey) & (order >= kOrderAgent) &&
                                (cls == kWallInner ? beats_wall(p.x, p.y, h.x, h.y, __uint_as_float(kv & ~kOrderMask))
                                                   : cls == kWallNone);
