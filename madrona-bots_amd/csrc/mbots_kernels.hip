@@ -1346,6 +1346,20 @@ __global__ __launch_bounds__(64 * kSensorWorlds, kCap <= 128 ? MB_SENSOR_BLOCKS 
             // others place each near point: inner / in a wall box / beyond.
             const bool deep = (p.x >= kInLo + 1.2f) & (p.x <= kInHiX - 1.2f) & (p.y >= kInLo + 1.2f) &
                               (p.y <= kInHiY - 1.2f);
+            // (one branch per lane: the wall class of its four near points)
+            int cls[4] = {kWallInner, kWallInner, kWallInner, kWallInner};
+            float s0[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+            if (!deep) {
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    const int k = 4 * g + t;
+                    const float c = R.c[k], sn = R.s[k];
+                    const float ex = c * h.x + sn * h.y, ey = c * h.y + sn * (-h.x);
+                    const float px = fw ? p.x + ex : p.x - ex, py = fw ? p.y + ey : p.y - ey;
+                    if (!inside_arena(px, py)) cls[t] = in_wall_box(px, py) ? kWallBox : kWallNone;
+                    s0[t] = c;
+                }
+            }
             uint32_t semv = 0, depv = 0;
 #pragma unroll
             for (int t = 0; t < 4; ++t) {
@@ -1354,26 +1368,14 @@ __global__ __launch_bounds__(64 * kSensorWorlds, kCap <= 128 ? MB_SENSOR_BLOCKS 
                 const uint32_t kv = kvs[t];
                 const float oz = __uint_as_float(kv & ~kOrderMask);
                 const uint32_t order = kv & kOrderMask;
-                int cls = kWallInner;
-                float s0 = 0.0f;
-                if (!deep) {
-                    const int k = 4 * g + t;
-                    const float c = R.c[k], sn = R.s[k];
-                    const float ex = c * h.x + sn * h.y, ey = c * h.y + sn * (-h.x);
-                    const float px = fw ? p.x + ex : p.x - ex, py = fw ? p.y + ey : p.y - ey;
-                    if (!inside_arena(px, py)) cls = in_wall_box(px, py) ? kWallBox : kWallNone;
-                    s0 = c;
-                }
-                const bool obj = (kv != kNoKey) &
-                                 (cls == kWallInner ? beats_wall(p.x, p.y, dx, dy, oz) : cls == kWallNone);
+                const bool inner = cls[t] == kWallInner, none = cls[t] == kWallNone;
+                const bool obj = (kv != kNoKey) & ((inner & beats_wall(p.x, p.y, dx, dy, oz)) | none);
                 // (any index in range: the species is used only for an agent's order)
                 const int spv = (int)L.sp[(order - kOrderAgent) & (kCap - 1)];
-                const int sem = obj ? (order < kOrderAgent ? 6 : spv) : (cls == kWallNone ? -1 : 5);
+                const int sem = obj ? (order < kOrderAgent ? 6 : spv) : (none ? -1 : 5);
                 semv |= (uint32_t)(uint8_t)(int8_t)sem << (8 * t);
                 if (depth) {
-                    const float z = obj ? oz
-                                  : cls == kWallInner ? wall_z(p.x, p.y, dx, dy)
-                                  : cls == kWallBox ? s0 : __builtin_inff();
+                    const float z = obj ? oz : inner ? wall_z(p.x, p.y, dx, dy) : none ? __builtin_inff() : s0[t];
                     depv |= (uint32_t)depth_u8(z) << (8 * t);
                 }
             }

@@ -204,27 +204,34 @@ MB_HD bool box_finder_hit(const FoodBox &b)
     return fabsf(b.l) <= fabsf(b.q) + fabsf(b.p);
 }
 
-// slab of one box axis along (1, u): lower / upper end of the ray parameter
-MB_HD float slab_lo(float m, float b)
+// The ray's exit from the square beyond the near sphere, after the line test:
+// forward, every slab's upper end >= s0 (the square's X span [f - ext, f + ext]
+// bounds the slab interval: wholly past s0 it is a hit, wholly before a miss);
+// backward, every slab's lower end <= -s0.  A slab (box coordinate s b - m,
+// m1 = f p + l q, m2 = l p - f q, b1 = p + u q, b2 = u p - q) ends past t iff
+// m + 1 >= t b (b > 0) / m - 1 <= t b (b < 0) -- multiplied out, no division.
+MB_HD bool slab_reaches(float m, float b, float t)
 {
-    return b > 0.0f ? (m - 1.0f) / b : b < 0.0f ? (m + 1.0f) / b : -__builtin_inff();
+    const float tb = t * b;
+    return b > 0.0f ? m + 1.0f >= tb : b < 0.0f ? m - 1.0f <= tb : true;
 }
-MB_HD float slab_hi(float m, float b)
+MB_HD bool slab_starts_before(float m, float b, float t)
 {
-    return b > 0.0f ? (m + 1.0f) / b : b < 0.0f ? (m - 1.0f) / b : __builtin_inff();
+    const float tb = t * b;
+    return b > 0.0f ? m - 1.0f <= tb : b < 0.0f ? m + 1.0f >= tb : true;
 }
 
-// the line test, then the ray's exit from the square beyond the near sphere:
-// forward hi >= s0, backward lo <= -s0, [lo, hi] the slabs' parameter interval
-// (box coordinates s b_i - m_i: m1 = f p + l q, m2 = l p - f q, b1 = p + u q,
-// b2 = u p - q); s0 = NearPt.c
+// the line test, then the exit beyond the near sphere (s0 = NearPt.c)
 MB_HD bool box_hit(const FoodBox &b, float u, bool fwd, float s0)
 {
     if (!box_line_hit(b, u)) return false;
+    const float zf = fwd ? b.f : -b.f;          // the square's centre along the ray
+    if (zf - b.ext >= s0) return true;          // wholly beyond the near point
+    if (zf + b.ext < s0) return false;          // wholly before it
     const float m1 = b.f * b.p + b.l * b.q, m2 = b.l * b.p - b.f * b.q;
     const float b1 = b.p + u * b.q, b2 = u * b.p - b.q;
-    if (fwd) return fmin_std(slab_hi(m1, b1), slab_hi(m2, b2)) >= s0;
-    return fmax_std(slab_lo(m1, b1), slab_lo(m2, b2)) <= -s0;
+    if (fwd) return (int)slab_reaches(m1, b1, s0) & (int)slab_reaches(m2, b2, s0);
+    return (int)slab_starts_before(m1, b1, -s0) & (int)slab_starts_before(m2, b2, -s0);
 }
 
 MB_HD float box_z(const FoodBox &b, bool fwd)

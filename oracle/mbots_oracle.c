@@ -698,7 +698,7 @@ static void food_cs(uint32_t q22, float *c, float *s)
  * the ray s (1, u) the square's slabs give the parameter interval [lo, hi]
  * (box coordinates s b_i - m_i, m1 = f p + l q, m2 = l p - f q, b1 = p + u q,
  * b2 = u p - q); a forward ray leaves it beyond the near sphere iff
- * hi >= s0, a backward one iff lo <= -s0 (s0 = 1.1 / |(1, u)|).  Depth (one
+ * hi >= s0, a backward one iff lo <= -s0 (s0 = 1.1 / |(1, u)|; box_hit).  Depth (one
  * per object, like the circles' f - R): the nearest corner's view depth,
  * max(0, f - (|p| + |q|)) forward, max(0, -(f + ...)) backward. */
 static int box_line_hit(float f, float l, float p, float q, float u)
@@ -706,28 +706,40 @@ static int box_line_hit(float f, float l, float p, float q, float u)
     return fabsf(l - u * f) <= fabsf(q - u * p) + fabsf(p + u * q);
 }
 
-/* slab of one box axis along direction (1, u): lower / upper end of s */
-static float slab_lo(float m, float b)
+/* A slab (box coordinate s b - m) ends past t iff m + 1 >= t b (b > 0) /
+ * m - 1 <= t b (b < 0); it starts before t iff m - 1 <= t b / m + 1 >= t b
+ * (always for b == 0, which the line test covers) -- the slab ends
+ * (m -+ 1) / b multiplied out. */
+static int slab_reaches(float m, float b, float t)
 {
-    if (b > 0.0f) return (m - 1.0f) / b;
-    if (b < 0.0f) return (m + 1.0f) / b;
-    return -INFINITY;
+    float tb = t * b;
+    if (b > 0.0f) return m + 1.0f >= tb;
+    if (b < 0.0f) return m - 1.0f <= tb;
+    return 1;
 }
 
-static float slab_hi(float m, float b)
+static int slab_starts_before(float m, float b, float t)
 {
-    if (b > 0.0f) return (m + 1.0f) / b;
-    if (b < 0.0f) return (m - 1.0f) / b;
-    return INFINITY;
+    float tb = t * b;
+    if (b > 0.0f) return m - 1.0f <= tb;
+    if (b < 0.0f) return m + 1.0f >= tb;
+    return 1;
 }
 
-static int box_hit(float f, float l, float p, float q, float u, int fwd, float s0)
+/* the line test, then the exit beyond the near point (ray parameter s0):
+ * the square's X span [f - ext, f + ext] along the ray bounds its slab
+ * interval -- wholly past s0 a hit, wholly before a miss -- else forward
+ * every slab must end past s0, backward every slab must start before -s0 */
+static int box_hit(float f, float l, float p, float q, float ext, float u, int fwd, float s0)
 {
     if (!box_line_hit(f, l, p, q, u)) return 0;
+    float zf = fwd ? f : -f;
+    if (zf - ext >= s0) return 1;
+    if (zf + ext < s0) return 0;
     float m1 = f * p + l * q, m2 = l * p - f * q;
     float b1 = p + u * q, b2 = u * p - q;
-    if (fwd) return fmin_std(slab_hi(m1, b1), slab_hi(m2, b2)) >= s0;
-    return fmax_std(slab_lo(m1, b1), slab_lo(m2, b2)) <= -s0;
+    if (fwd) return slab_reaches(m1, b1, s0) && slab_reaches(m2, b2, s0);
+    return slab_starts_before(m1, b1, -s0) && slab_starts_before(m2, b2, -s0);
 }
 
 static void raster_box(orc_hit *hits, float ax, float ay, float hx, float hy, float cx, float cy,
@@ -746,7 +758,7 @@ static void raster_box(orc_hit *hits, float ax, float ay, float hx, float hy, fl
         int fwd = k < 24 || k == ORC_SENSOR;
         float nc, ns, ne;
         near_pt(k, &nc, &ns, &ne);
-        if (box_hit(f, l, p, q, ray_u(k), fwd, nc)) consider(&hits[k], fwd ? zf : zb, order);
+        if (box_hit(f, l, p, q, ext, ray_u(k), fwd, nc)) consider(&hits[k], fwd ? zf : zb, order);
     }
 }
 
