@@ -1111,11 +1111,13 @@ __device__ __forceinline__ void run_survivors(LDS &L, const RayTab &R, int nf, i
     const uint64_t wm = ballot64(wide);
     if (wide) L.qcode[q0 + (int)rank_below(wm)] = code;
     const int nw = __popcll(wm);
+#ifndef MB_SKIP_WIDE   // (instruction-count probes only: MB_SKIP_* builds give wrong rows)
     if (nw > 0) {
         wave_sync();
         run_wide(L, R, nf, a0, q0, nw);
         wave_sync();
     }
+#endif
 }
 
 // the world's staged inputs, loaded as one batch of independent loads
@@ -1306,16 +1308,21 @@ __global__ __launch_bounds__(64 * kSensorWorlds, kCap <= 128 ? MB_SENSOR_BLOCKS 
                 nq += __popcll(m);
                 if (nq >= 64) {
                     wave_sync();
+#ifndef MB_SKIP_P2
                     run_survivors(L, R, nf, a0, nq - 64, 64);
+#endif
                     nq -= 64;
                 }
             }
         }
         if (nq > 0) {
             wave_sync();
+#ifndef MB_SKIP_P2
             run_survivors(L, R, nf, a0, 0, nq);
+#endif
         }
         wave_sync();
+#ifndef MB_SKIP_OUT
         // ---- output: keys vs walls; lane = (agent ci, pixels 4g .. 4g+3) ----
         {
             const int ci = (int)(lane >> 3), g = (int)(lane & 7u);
@@ -1416,6 +1423,7 @@ __global__ __launch_bounds__(64 * kSensorWorlds, kCap <= 128 ? MB_SENSOR_BLOCKS 
                                                   : cls == kWallNone);
             S.finder[base + i] = agent ? (int32_t)(order - kOrderAgent) : -1;
         }
+#endif
         wave_sync();
     }
     }
