@@ -1351,53 +1351,43 @@ __global__ __launch_bounds__(64 * kSensorWorlds, kCap <= 128 ? MB_SENSOR_BLOCKS 
             // an agent 1.2 inside the inner rectangle has every ray's near point
             // (1.1 from it) in the rectangle: the wall is the exit from it.  The
             // others place each near point: inner / in a wall box / beyond.
+#ifdef MB_PROBE_ALL_DEEP   // (instruction-count probe: wrong rows near the walls)
+            const bool deep = true;
+#else
             const bool deep = (p.x >= kInLo + 1.2f) & (p.x <= kInHiX - 1.2f) & (p.y >= kInLo + 1.2f) &
                               (p.y <= kInHiY - 1.2f);
-            uint32_t semv = 0, depv = 0;
-            if (ballot64(!deep) == 0ull) {
-                // every lane's agent is deep (a wave-uniform branch, ~half the
-                // chunks): the wall is each ray's exit from the inner rectangle
+#endif
+            // (one branch per lane: the wall class of its four near points)
+            int cls[4] = {kWallInner, kWallInner, kWallInner, kWallInner};
+            float s0[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+            if (!deep) {
 #pragma unroll
                 for (int t = 0; t < 4; ++t) {
-                    const float u = us[t];
-                    const float dx = hxs + u * hys, dy = hys + u * (-hxs);
-                    const uint32_t kv = kvs[t];
-                    const float oz = __uint_as_float(kv & ~kOrderMask);
-                    const uint32_t order = kv & kOrderMask;
-                    const bool obj = (kv != kNoKey) & beats_wall(p.x, p.y, dx, dy, oz);
-                    // (any index in range: the species is used only for an agent's order)
-                    const int spv = (int)L.sp[(order - kOrderAgent) & (kCap - 1)];
-                    const int sem = obj ? (order < kOrderAgent ? 6 : spv) : 5;
-                    semv |= (uint32_t)(uint8_t)(int8_t)sem << (8 * t);
-                    if (depth) {
-                        const float z = obj ? oz : wall_z(p.x, p.y, dx, dy);
-                        depv |= (uint32_t)depth_u8(z) << (8 * t);
-                    }
-                }
-            } else {
-                // some agent within 1.2 of the inner rectangle's edge: place each
-                // ray's near point (inner / in a wall box / beyond the walls)
-#pragma unroll
-                for (int t = 0; t < 4; ++t) {
-                    const float u = us[t];
-                    const float dx = hxs + u * hys, dy = hys + u * (-hxs);
-                    const uint32_t kv = kvs[t];
-                    const float oz = __uint_as_float(kv & ~kOrderMask);
-                    const uint32_t order = kv & kOrderMask;
                     const int k = 4 * g + t;
                     const float c = R.c[k], sn = R.s[k];
                     const float ex = c * h.x + sn * h.y, ey = c * h.y + sn * (-h.x);
                     const float px = fw ? p.x + ex : p.x - ex, py = fw ? p.y + ey : p.y - ey;
-                    const bool inner = inside_arena(px, py);
-                    const bool none = !inner & !in_wall_box(px, py);
-                    const bool obj = (kv != kNoKey) & ((inner & beats_wall(p.x, p.y, dx, dy, oz)) | none);
-                    const int spv = (int)L.sp[(order - kOrderAgent) & (kCap - 1)];
-                    const int sem = obj ? (order < kOrderAgent ? 6 : spv) : (none ? -1 : 5);
-                    semv |= (uint32_t)(uint8_t)(int8_t)sem << (8 * t);
-                    if (depth) {
-                        const float z = obj ? oz : inner ? wall_z(p.x, p.y, dx, dy) : none ? __builtin_inff() : c;
-                        depv |= (uint32_t)depth_u8(z) << (8 * t);
-                    }
+                    if (!inside_arena(px, py)) cls[t] = in_wall_box(px, py) ? kWallBox : kWallNone;
+                    s0[t] = c;
+                }
+            }
+            uint32_t semv = 0, depv = 0;
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const float u = us[t];
+                const float dx = hxs + u * hys, dy = hys + u * (-hxs);
+                const uint32_t kv = kvs[t];
+                const float oz = __uint_as_float(kv & ~kOrderMask);
+                const uint32_t order = kv & kOrderMask;
+                const bool inner = cls[t] == kWallInner, none = cls[t] == kWallNone;
+                const bool obj = (kv != kNoKey) & ((inner & beats_wall(p.x, p.y, dx, dy, oz)) | none);
+                // (any index in range: the species is used only for an agent's order)
+                const int spv = (int)L.sp[(order - kOrderAgent) & (kCap - 1)];
+                const int sem = obj ? (order < kOrderAgent ? 6 : spv) : (none ? -1 : 5);
+                semv |= (uint32_t)(uint8_t)(int8_t)sem << (8 * t);
+                if (depth) {
+                    const float z = obj ? oz : inner ? wall_z(p.x, p.y, dx, dy) : none ? __builtin_inff() : s0[t];
+                    depv |= (uint32_t)depth_u8(z) << (8 * t);
                 }
             }
             if (ci < nc) {
@@ -1413,11 +1403,18 @@ __global__ __launch_bounds__(64 * kSensorWorlds, kCap <= 128 ? MB_SENSOR_BLOCKS 
             const uint32_t order = kv & kOrderMask;
             // the centre ray's near point (1.1 ahead): in the inner rectangle
             // unless the agent is within 1.1 of its edge
+#ifdef MB_PROBE_ALL_DEEP
+            const bool deep = true;
+#else
+            const bool deep = (p.x >= kInLo + 1.2f) & (p.x <= kInHiX - 1.2f) & (p.y >= kInLo + 1.2f) &
+                              (p.y <= kInHiY - 1.2f);
+#endif
             int cls = kWallInner;
-            const float c = R.c[kSensor], sn = R.s[kSensor];
-            const float ex = c * h.x + sn * h.y, ey = c * h.y + sn * (-h.x);
-            const float px = p.x + ex, py = p.y + ey;
-            if (!inside_arena(px, py)) cls = in_wall_box(px, py) ? kWallBox : kWallNone;
+            if (!deep) {
+                const float c = R.c[kSensor], sn = R.s[kSensor];
+                const float ex = c * h.x + sn * h.y, ey = c * h.y + sn * (-h.x);
+                cls = wall_class(p.x + ex, p.y + ey);
+            }
             const bool agent = (kv != kNoKey) & (order >= kOrderAgent) &&
                                (cls == kWallInner ? beats_wall(p.x, p.y, h.x, h.y, __uint_as_float(kv & ~kOrderMask))
                                                   : cls == kWallNone);
