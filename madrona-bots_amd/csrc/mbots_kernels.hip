@@ -938,13 +938,15 @@ constexpr float kFarCull = 5.0f;               // P1 angular cull from this |f| 
 
 template <int kCap>
 struct SensorLDS {
-    // positions: food, then agents, then (kCap <= 128) 64 NaN sentinels that P1
+    // positions: food, then agents, then (kCap <= 128) 32 NaN sentinels that P1
     // reads past nobj unchecked (the 256-slot class keeps its bounds checks: 2 KB
     // more per block would cost it a block per CU)
-    float2 obj[kMaxFood + kCap + (kCap <= 128 ? 64 : 0)];
+    float2 obj[kMaxFood + kCap + (kCap <= 128 ? 32 : 0)];
     float2 frot[kMaxFood];                    // food squares' (cos, sin)
     float2 hd[kCap];                          // agent headings
     int8_t sp[kCap];
+    uint8_t ord[kCap];                        // chunk order of the agents: slots with every
+                                              // ray's near point inside the arena first
     alignas(16) uint32_t key[kKeyAgents * kKeyStride];
     uint32_t qcode[kQueueCap + 1];            // P1 survivors: agent | object << 11 (+ a
                                               // sink slot for the branch-free write); a
@@ -1002,11 +1004,12 @@ __device__ __forceinline__ void run_wide(LDS &L, const RayTab &R, int nf, int a0
             const int ic = (int)(code & 0x1Fu), j = (int)(code >> 11);
             float f, l;
             uint32_t order;
-            pair_fl(L, nf, a0 + ic, j, f, l, order);
+            const int ia = L.ord[a0 + ic];
+            pair_fl(L, nf, ia, j, f, l, order);
             uint32_t *kr = L.key + ic * kKeyStride;
             uint32_t kv, kf;
             if (j < nf) {   // food square: every ray exactly
-                const FoodBox b = box_setup(f, l, L.frot[j], L.hd[a0 + ic]);
+                const FoodBox b = box_setup(f, l, L.frot[j], L.hd[ia]);
                 kv = box_hit(b, uk, k < 24, np.c) ? zkey(box_z(b, k < 24), order) : kNoKey;
                 kf = box_hit(b, 0.0f, true, fnp.c) ? zkey(box_z(b, true), order) : kNoKey;
             } else {
@@ -1033,7 +1036,8 @@ __device__ __forceinline__ void run_survivors(LDS &L, const RayTab &R, int nf, i
         code = L.qcode[q0 + lane];
         const int ic = (int)(code & 0x1Fu), j = (int)(code >> 11);
         uint32_t order;
-        pair_fl(L, nf, a0 + ic, j, f, l, order);
+        const int ia = L.ord[a0 + ic];
+        pair_fl(L, nf, ia, j, f, l, order);
         const bool food = j < nf;
         const float r2 = f * f + l * l;
         if ((fabsf(f) <= (food ? kFoodFar : 1.5f)) | (r2 <= (food ? kFoodFar2 : kCircleFar2))) {
@@ -1051,7 +1055,7 @@ __device__ __forceinline__ void run_survivors(LDS &L, const RayTab &R, int nf, i
             float ulo, uhi;
             FoodBox b{};
             if (food) {
-                b = box_setup(f, l, L.frot[j], L.hd[a0 + ic]);
+                b = box_setup(f, l, L.frot[j], L.hd[ia]);
                 // corner offsets +-(p - q, p + q), +-(p + q, q - p)
                 const float ax = b.p - b.q, ay = b.p + b.q;
                 const float s0 = (l + ay) * __builtin_amdgcn_rcpf(f + ax);
@@ -1241,11 +1245,48 @@ __global__ __launch_bounds__(64 * kSensorWorlds, kCap <= 128 ? MB_SENSOR_BLOCKS 
                 : sp == 3 ? rb.z + c3 + (int)rank_below(m3) : rb.w + c4 + (int)rank_below(m4);
         c1 += __popcll(m1); c2 += __popcll(m2); c3 += __popcll(m3); c4 += __popcll(m4);
     }
+    // chunk order: agents whose every ray's near point lies in the inner
+    // rectangle ("deep", 1.2 inside it) first, in slot order, then the others,
+    // so the output pass's wall-class work (near the walls) falls in as few
+    // chunks as possible (the results do not depend on the order)
+    {
+        int dbase = 0;
+#pragma unroll
+        for (int g = 0; g < kG; ++g) {
+            if (g > 0 && 64 * g >= n) break;
+            const int i = 64 * g + (int)lane;
+            bool dp = false;
+            if (i < n) {
+                const float2 q = L.obj[nf + i];
+                dp = (q.x >= kInLo + 1.2f) & (q.x <= kInHiX - 1.2f) & (q.y >= kInLo + 1.2f) &
+                     (q.y <= kInHiY - 1.2f);
+            }
+            dbase += __popcll(ballot64(dp));
+        }
+        int dseen = 0, nseen = 0;
+#pragma unroll
+        for (int g = 0; g < kG; ++g) {
+            if (g > 0 && 64 * g >= n) break;
+            const int i = 64 * g + (int)lane;
+            const bool valid = i < n;
+            bool dp = false;
+            if (valid) {
+                const float2 q = L.obj[nf + i];
+                dp = (q.x >= kInLo + 1.2f) & (q.x <= kInHiX - 1.2f) & (q.y >= kInLo + 1.2f) &
+                     (q.y <= kInHiY - 1.2f);
+            }
+            const uint64_t md = ballot64(valid & dp), mn = ballot64(valid & !dp);
+            if (valid) L.ord[dp ? dseen + (int)rank_below(md) : dbase + nseen + (int)rank_below(mn)] = (uint8_t)i;
+            dseen += __popcll(md);
+            nseen += __popcll(mn);
+        }
+    }
     const int nobj = nf + n;
     // sentinels past the last object: a NaN position fails every P1 test, so
-    // the pair loop needs no bounds check or clamped read (j < nobj + 63)
+    // the pair loop needs no bounds check or clamped read (j < nobj + 31: P1
+    // takes at least two agents' lanes per object group, G <= 32)
     constexpr bool kPad = kCap <= 128;
-    if (kPad) L.obj[nobj + (int)lane] = make_float2(__builtin_nanf(""), __builtin_nanf(""));
+    if (kPad && lane < 32) L.obj[nobj + (int)lane] = make_float2(__builtin_nanf(""), __builtin_nanf(""));
     wave_sync();
 
     for (int a0 = kChunk0; a0 < n; a0 += kChunkStep) {
@@ -1257,10 +1298,10 @@ __global__ __launch_bounds__(64 * kSensorWorlds, kCap <= 128 ? MB_SENSOR_BLOCKS 
         // 2, 4 or 8 and G = 64 / P object groups, objects j = o + G t ----
         int nq = 0;
         {
-            const int P = nc > 4 ? 8 : nc > 2 ? 4 : nc > 1 ? 2 : 1;
-            const int G = 64 / P, lgG = 6 - (P == 8 ? 3 : P == 4 ? 2 : P == 2 ? 1 : 0);
+            const int P = nc > 4 ? 8 : nc > 2 ? 4 : 2;   // (P >= 2: the sentinels cover G <= 32)
+            const int G = 64 / P, lgG = 6 - (P == 8 ? 3 : P == 4 ? 2 : 1);
             const int a = (int)lane >> lgG, o = (int)lane & (G - 1);
-            const int ia = a0 + min(a, nc - 1);
+            const int ia = L.ord[a0 + min(a, nc - 1)];
             // a lane past the chunk's agents gets a NaN camera: every test fails
             const float2 ap = a < nc ? L.obj[nf + ia] : make_float2(__builtin_nanf(""), __builtin_nanf(""));
             const float2 ah = L.hd[ia];
@@ -1327,19 +1368,16 @@ __global__ __launch_bounds__(64 * kSensorWorlds, kCap <= 128 ? MB_SENSOR_BLOCKS 
         {
             const int ci = (int)(lane >> 3), g = (int)(lane & 7u);
             const int cc = min(ci, nc - 1);
-            const int i = a0 + cc;
+            const int i = L.ord[a0 + cc];   // the agent's slot
             const float2 p = L.obj[nf + i], h = L.hd[i];
             const uint4 kv4 = *reinterpret_cast<const uint4 *>(&L.key[cc * kKeyStride + 4 * g]);
             const float4 u4 = *reinterpret_cast<const float4 *>(&R.u[4 * g]);
-            // the chunk's 64-slot group (8 | 64: one group per chunk), a uniform branch
-            int r;
-            if constexpr (kG == 2) {
-                r = a0 < 64 ? __shfl(rows[0], i & 63) : __shfl(rows[1], i & 63);
-            } else {
-                r = __shfl(rows[0], i & 63);
+            // the slot's row: lane s of rows[g] holds slot 64 g + s
+            int r = __shfl(rows[0], i & 63);
 #pragma unroll
-                for (int g = 1; g < kG; ++g)
-                    if ((a0 >> 6) == g) r = __shfl(rows[g], i & 63);
+            for (int g = 1; g < kG; ++g) {
+                const int rg = __shfl(rows[g], i & 63);
+                if ((i >> 6) == g) r = rg;
             }
             // backward pixels look along -(h + u r): the sign folded into the
             // heading, sgn (h.x + u h.y) == (sgn h.x) + u (sgn h.y) exactly (IEEE
@@ -1397,7 +1435,7 @@ __global__ __launch_bounds__(64 * kSensorWorlds, kCap <= 128 ? MB_SENSOR_BLOCKS 
             }
         }
         if ((int)lane < nc) {
-            const int i = a0 + (int)lane;
+            const int i = L.ord[a0 + (int)lane];
             const float2 p = L.obj[nf + i], h = L.hd[i];
             const uint32_t kv = L.key[lane * kKeyStride + kSensor];
             const uint32_t order = kv & kOrderMask;
