@@ -987,16 +987,18 @@ __device__ __forceinline__ void pair_fl(const LDS &L, int nf, int i, int j, floa
     l = vx * h.y - vy * h.x;   // along r = (hy, -hx)
 }
 
-// W: wide pairs qcode[q0, q0 + cnt), two per wave (32 lanes each: rays 0..31,
-// lane 0 of each half also takes the finder ray)
-template <class LDS>
+// W: wide pairs qcode[q0, q0 + cnt) of one kind (kFood: food squares, else
+// agent discs), two per wave (32 lanes each: rays 0..31, lane 0 of each half
+// also takes the finder ray); one kind per call, so a wave never runs both
+// kinds' predicates for one pair
+template <bool kFood, class LDS>
 __device__ __forceinline__ void run_wide(LDS &L, const RayTab &R, int nf, int a0, int q0, int cnt)
 {
     const int lane = (int)__lane_id();
     // ray k's offset and near point (the near sphere): loop invariant
     const int k = lane & 31;
     const float uk = R.u[k];
-    const NearPt np{R.c[k], R.s[k], R.e[k]}, fnp{R.c[kSensor], R.s[kSensor], R.e[kSensor]};
+    const NearPt np{R.c[k], R.s[k], R.e[k]};
     for (int e0 = 0; e0 < cnt; e0 += 2) {
         const int e = e0 + (lane >> 5);
         if (e < cnt) {
@@ -1008,10 +1010,10 @@ __device__ __forceinline__ void run_wide(LDS &L, const RayTab &R, int nf, int a0
             pair_fl(L, nf, ia, j, f, l, order);
             uint32_t *kr = L.key + ic * kKeyStride;
             uint32_t kv, kf;
-            if (j < nf) {   // food square: every ray exactly
+            if constexpr (kFood) {   // food square: every ray exactly
                 const FoodBox b = box_setup(f, l, L.frot[j], L.hd[ia]);
                 kv = box_hit(b, uk, k < 24, np.c) ? zkey(box_z(b, k < 24), order) : kNoKey;
-                kf = box_hit(b, 0.0f, true, fnp.c) ? zkey(box_z(b, true), order) : kNoKey;
+                kf = box_hit(b, 0.0f, true, R.c[kSensor]) ? zkey(box_z(b, true), order) : kNoKey;
             } else {
                 kv = pixel_key(f, l, uk, np, k < 24, order);
                 kf = finder_key(f, l, order);
@@ -1111,14 +1113,17 @@ __device__ __forceinline__ void run_survivors(LDS &L, const RayTab &R, int nf, i
             for (int k = k0 + 1; k < kl; ++k) atomicMin(&kr[k], kin);
         }
     }
-    // every lane read its code above: the wide ones compact in place
-    const uint64_t wm = ballot64(wide);
-    if (wide) L.qcode[q0 + (int)rank_below(wm)] = code;
-    const int nw = __popcll(wm);
+    // every lane read its code above: the wide ones compact in place, food
+    // squares first, then discs
+    const bool wfood = wide & ((int)(code >> 11) < nf);
+    const uint64_t wf = ballot64(wfood), wc = ballot64(wide & !wfood);
+    const int nwf = __popcll(wf), nwc = __popcll(wc);
+    if (wide) L.qcode[q0 + (wfood ? (int)rank_below(wf) : nwf + (int)rank_below(wc))] = code;
 #ifndef MB_SKIP_WIDE   // (instruction-count probes only: MB_SKIP_* builds give wrong rows)
-    if (nw > 0) {
+    if (nwf + nwc > 0) {
         wave_sync();
-        run_wide(L, R, nf, a0, q0, nw);
+        if (nwf > 0) run_wide<true>(L, R, nf, a0, q0, nwf);
+        if (nwc > 0) run_wide<false>(L, R, nf, a0, q0 + nwf, nwc);
         wave_sync();
     }
 #endif
