@@ -938,15 +938,13 @@ constexpr float kFarCull = 5.0f;               // P1 angular cull from this |f| 
 
 template <int kCap>
 struct SensorLDS {
-    // positions: food, then agents, then (kCap <= 128) 32 NaN sentinels that P1
+    // positions: food, then agents, then (kCap <= 128) 64 NaN sentinels that P1
     // reads past nobj unchecked (the 256-slot class keeps its bounds checks: 2 KB
     // more per block would cost it a block per CU)
-    float2 obj[kMaxFood + kCap + (kCap <= 128 ? 32 : 0)];
+    float2 obj[kMaxFood + kCap + (kCap <= 128 ? 64 : 0)];
     float2 frot[kMaxFood];                    // food squares' (cos, sin)
     float2 hd[kCap];                          // agent headings
     int8_t sp[kCap];
-    uint8_t ord[kCap];                        // chunk order of the agents: slots with every
-                                              // ray's near point inside the arena first
     alignas(16) uint32_t key[kKeyAgents * kKeyStride];
     uint32_t qcode[kQueueCap + 1];            // P1 survivors: agent | object << 11 (+ a
                                               // sink slot for the branch-free write); a
@@ -987,18 +985,16 @@ __device__ __forceinline__ void pair_fl(const LDS &L, int nf, int i, int j, floa
     l = vx * h.y - vy * h.x;   // along r = (hy, -hx)
 }
 
-// W: wide pairs qcode[q0, q0 + cnt) of one kind (kFood: food squares, else
-// agent discs), two per wave (32 lanes each: rays 0..31, lane 0 of each half
-// also takes the finder ray); one kind per call, so a wave never runs both
-// kinds' predicates for one pair
-template <bool kFood, class LDS>
+// W: wide pairs qcode[q0, q0 + cnt), two per wave (32 lanes each: rays 0..31,
+// lane 0 of each half also takes the finder ray)
+template <class LDS>
 __device__ __forceinline__ void run_wide(LDS &L, const RayTab &R, int nf, int a0, int q0, int cnt)
 {
     const int lane = (int)__lane_id();
     // ray k's offset and near point (the near sphere): loop invariant
     const int k = lane & 31;
     const float uk = R.u[k];
-    const NearPt np{R.c[k], R.s[k], R.e[k]};
+    const NearPt np{R.c[k], R.s[k], R.e[k]}, fnp{R.c[kSensor], R.s[kSensor], R.e[kSensor]};
     for (int e0 = 0; e0 < cnt; e0 += 2) {
         const int e = e0 + (lane >> 5);
         if (e < cnt) {
@@ -1006,14 +1002,13 @@ __device__ __forceinline__ void run_wide(LDS &L, const RayTab &R, int nf, int a0
             const int ic = (int)(code & 0x1Fu), j = (int)(code >> 11);
             float f, l;
             uint32_t order;
-            const int ia = L.ord[a0 + ic];
-            pair_fl(L, nf, ia, j, f, l, order);
+            pair_fl(L, nf, a0 + ic, j, f, l, order);
             uint32_t *kr = L.key + ic * kKeyStride;
             uint32_t kv, kf;
-            if constexpr (kFood) {   // food square: every ray exactly
-                const FoodBox b = box_setup(f, l, L.frot[j], L.hd[ia]);
+            if (j < nf) {   // food square: every ray exactly
+                const FoodBox b = box_setup(f, l, L.frot[j], L.hd[a0 + ic]);
                 kv = box_hit(b, uk, k < 24, np.c) ? zkey(box_z(b, k < 24), order) : kNoKey;
-                kf = box_hit(b, 0.0f, true, R.c[kSensor]) ? zkey(box_z(b, true), order) : kNoKey;
+                kf = box_hit(b, 0.0f, true, fnp.c) ? zkey(box_z(b, true), order) : kNoKey;
             } else {
                 kv = pixel_key(f, l, uk, np, k < 24, order);
                 kf = finder_key(f, l, order);
@@ -1038,8 +1033,7 @@ __device__ __forceinline__ void run_survivors(LDS &L, const RayTab &R, int nf, i
         code = L.qcode[q0 + lane];
         const int ic = (int)(code & 0x1Fu), j = (int)(code >> 11);
         uint32_t order;
-        const int ia = L.ord[a0 + ic];
-        pair_fl(L, nf, ia, j, f, l, order);
+        pair_fl(L, nf, a0 + ic, j, f, l, order);
         const bool food = j < nf;
         const float r2 = f * f + l * l;
         if ((fabsf(f) <= (food ? kFoodFar : 1.5f)) | (r2 <= (food ? kFoodFar2 : kCircleFar2))) {
@@ -1057,7 +1051,7 @@ __device__ __forceinline__ void run_survivors(LDS &L, const RayTab &R, int nf, i
             float ulo, uhi;
             FoodBox b{};
             if (food) {
-                b = box_setup(f, l, L.frot[j], L.hd[ia]);
+                b = box_setup(f, l, L.frot[j], L.hd[a0 + ic]);
                 // corner offsets +-(p - q, p + q), +-(p + q, q - p)
                 const float ax = b.p - b.q, ay = b.p + b.q;
                 const float s0 = (l + ay) * __builtin_amdgcn_rcpf(f + ax);
@@ -1113,17 +1107,14 @@ __device__ __forceinline__ void run_survivors(LDS &L, const RayTab &R, int nf, i
             for (int k = k0 + 1; k < kl; ++k) atomicMin(&kr[k], kin);
         }
     }
-    // every lane read its code above: the wide ones compact in place, food
-    // squares first, then discs
-    const bool wfood = wide & ((int)(code >> 11) < nf);
-    const uint64_t wf = ballot64(wfood), wc = ballot64(wide & !wfood);
-    const int nwf = __popcll(wf), nwc = __popcll(wc);
-    if (wide) L.qcode[q0 + (wfood ? (int)rank_below(wf) : nwf + (int)rank_below(wc))] = code;
+    // every lane read its code above: the wide ones compact in place
+    const uint64_t wm = ballot64(wide);
+    if (wide) L.qcode[q0 + (int)rank_below(wm)] = code;
+    const int nw = __popcll(wm);
 #ifndef MB_SKIP_WIDE   // (instruction-count probes only: MB_SKIP_* builds give wrong rows)
-    if (nwf + nwc > 0) {
+    if (nw > 0) {
         wave_sync();
-        if (nwf > 0) run_wide<true>(L, R, nf, a0, q0, nwf);
-        if (nwc > 0) run_wide<false>(L, R, nf, a0, q0 + nwf, nwc);
+        run_wide(L, R, nf, a0, q0, nw);
         wave_sync();
     }
 #endif
@@ -1250,48 +1241,11 @@ __global__ __launch_bounds__(64 * kSensorWorlds, kCap <= 128 ? MB_SENSOR_BLOCKS 
                 : sp == 3 ? rb.z + c3 + (int)rank_below(m3) : rb.w + c4 + (int)rank_below(m4);
         c1 += __popcll(m1); c2 += __popcll(m2); c3 += __popcll(m3); c4 += __popcll(m4);
     }
-    // chunk order: agents whose every ray's near point lies in the inner
-    // rectangle ("deep", 1.2 inside it) first, in slot order, then the others,
-    // so the output pass's wall-class work (near the walls) falls in as few
-    // chunks as possible (the results do not depend on the order)
-    {
-        int dbase = 0;
-#pragma unroll
-        for (int g = 0; g < kG; ++g) {
-            if (g > 0 && 64 * g >= n) break;
-            const int i = 64 * g + (int)lane;
-            bool dp = false;
-            if (i < n) {
-                const float2 q = L.obj[nf + i];
-                dp = (q.x >= kInLo + 1.2f) & (q.x <= kInHiX - 1.2f) & (q.y >= kInLo + 1.2f) &
-                     (q.y <= kInHiY - 1.2f);
-            }
-            dbase += __popcll(ballot64(dp));
-        }
-        int dseen = 0, nseen = 0;
-#pragma unroll
-        for (int g = 0; g < kG; ++g) {
-            if (g > 0 && 64 * g >= n) break;
-            const int i = 64 * g + (int)lane;
-            const bool valid = i < n;
-            bool dp = false;
-            if (valid) {
-                const float2 q = L.obj[nf + i];
-                dp = (q.x >= kInLo + 1.2f) & (q.x <= kInHiX - 1.2f) & (q.y >= kInLo + 1.2f) &
-                     (q.y <= kInHiY - 1.2f);
-            }
-            const uint64_t md = ballot64(valid & dp), mn = ballot64(valid & !dp);
-            if (valid) L.ord[dp ? dseen + (int)rank_below(md) : dbase + nseen + (int)rank_below(mn)] = (uint8_t)i;
-            dseen += __popcll(md);
-            nseen += __popcll(mn);
-        }
-    }
     const int nobj = nf + n;
     // sentinels past the last object: a NaN position fails every P1 test, so
-    // the pair loop needs no bounds check or clamped read (j < nobj + 31: P1
-    // takes at least two agents' lanes per object group, G <= 32)
+    // the pair loop needs no bounds check or clamped read (j < nobj + 63)
     constexpr bool kPad = kCap <= 128;
-    if (kPad && lane < 32) L.obj[nobj + (int)lane] = make_float2(__builtin_nanf(""), __builtin_nanf(""));
+    if (kPad) L.obj[nobj + (int)lane] = make_float2(__builtin_nanf(""), __builtin_nanf(""));
     wave_sync();
 
     for (int a0 = kChunk0; a0 < n; a0 += kChunkStep) {
@@ -1303,10 +1257,10 @@ __global__ __launch_bounds__(64 * kSensorWorlds, kCap <= 128 ? MB_SENSOR_BLOCKS 
         // 2, 4 or 8 and G = 64 / P object groups, objects j = o + G t ----
         int nq = 0;
         {
-            const int P = nc > 4 ? 8 : nc > 2 ? 4 : 2;   // (P >= 2: the sentinels cover G <= 32)
-            const int G = 64 / P, lgG = 6 - (P == 8 ? 3 : P == 4 ? 2 : 1);
+            const int P = nc > 4 ? 8 : nc > 2 ? 4 : nc > 1 ? 2 : 1;
+            const int G = 64 / P, lgG = 6 - (P == 8 ? 3 : P == 4 ? 2 : P == 2 ? 1 : 0);
             const int a = (int)lane >> lgG, o = (int)lane & (G - 1);
-            const int ia = L.ord[a0 + min(a, nc - 1)];
+            const int ia = a0 + min(a, nc - 1);
             // a lane past the chunk's agents gets a NaN camera: every test fails
             const float2 ap = a < nc ? L.obj[nf + ia] : make_float2(__builtin_nanf(""), __builtin_nanf(""));
             const float2 ah = L.hd[ia];
@@ -1373,16 +1327,19 @@ __global__ __launch_bounds__(64 * kSensorWorlds, kCap <= 128 ? MB_SENSOR_BLOCKS 
         {
             const int ci = (int)(lane >> 3), g = (int)(lane & 7u);
             const int cc = min(ci, nc - 1);
-            const int i = L.ord[a0 + cc];   // the agent's slot
+            const int i = a0 + cc;
             const float2 p = L.obj[nf + i], h = L.hd[i];
             const uint4 kv4 = *reinterpret_cast<const uint4 *>(&L.key[cc * kKeyStride + 4 * g]);
             const float4 u4 = *reinterpret_cast<const float4 *>(&R.u[4 * g]);
-            // the slot's row: lane s of rows[g] holds slot 64 g + s
-            int r = __shfl(rows[0], i & 63);
+            // the chunk's 64-slot group (8 | 64: one group per chunk), a uniform branch
+            int r;
+            if constexpr (kG == 2) {
+                r = a0 < 64 ? __shfl(rows[0], i & 63) : __shfl(rows[1], i & 63);
+            } else {
+                r = __shfl(rows[0], i & 63);
 #pragma unroll
-            for (int g = 1; g < kG; ++g) {
-                const int rg = __shfl(rows[g], i & 63);
-                if ((i >> 6) == g) r = rg;
+                for (int g = 1; g < kG; ++g)
+                    if ((a0 >> 6) == g) r = __shfl(rows[g], i & 63);
             }
             // backward pixels look along -(h + u r): the sign folded into the
             // heading, sgn (h.x + u h.y) == (sgn h.x) + u (sgn h.y) exactly (IEEE
@@ -1391,29 +1348,14 @@ __global__ __launch_bounds__(64 * kSensorWorlds, kCap <= 128 ? MB_SENSOR_BLOCKS 
             const float hxs = fw ? h.x : -h.x, hys = fw ? h.y : -h.y;
             const uint32_t kvs[4] = {kv4.x, kv4.y, kv4.z, kv4.w};
             const float us[4] = {u4.x, u4.y, u4.z, u4.w};
-            // an agent 1.2 inside the inner rectangle has every ray's near point
-            // (1.1 from it) in the rectangle: the wall is the exit from it.  The
-            // others place each near point: inner / in a wall box / beyond.
-#ifdef MB_PROBE_ALL_DEEP   // (instruction-count probe: wrong rows near the walls)
-            const bool deep = true;
-#else
-            const bool deep = (p.x >= kInLo + 1.2f) & (p.x <= kInHiX - 1.2f) & (p.y >= kInLo + 1.2f) &
-                              (p.y <= kInHiY - 1.2f);
-#endif
-            // (one branch per lane: the wall class of its four near points)
-            int cls[4] = {kWallInner, kWallInner, kWallInner, kWallInner};
-            float s0[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-            if (!deep) {
-#pragma unroll
-                for (int t = 0; t < 4; ++t) {
-                    const int k = 4 * g + t;
-                    const float c = R.c[k], sn = R.s[k];
-                    const float ex = c * h.x + sn * h.y, ey = c * h.y + sn * (-h.x);
-                    const float px = fw ? p.x + ex : p.x - ex, py = fw ? p.y + ey : p.y - ey;
-                    if (!inside_arena(px, py)) cls[t] = in_wall_box(px, py) ? kWallBox : kWallNone;
-                    s0[t] = c;
-                }
-            }
+            // each ray's near point P0 = o + c d: from an origin
+            // inside the inner rectangle it lies inside iff the ray's exit lies
+            // beyond view depth c -- the walls' per-axis test at z = c; the rest
+            // (an origin in a wall band, a ray leaving the rectangle within the
+            // near sphere) place P0 itself, a branch few waves take
+            const float4 c4 = *reinterpret_cast<const float4 *>(&R.c[4 * g]);
+            const float cs[4] = {c4.x, c4.y, c4.z, c4.w};
+            const bool oin = inside_arena(p.x, p.y);
             uint32_t semv = 0, depv = 0;
 #pragma unroll
             for (int t = 0; t < 4; ++t) {
@@ -1422,14 +1364,22 @@ __global__ __launch_bounds__(64 * kSensorWorlds, kCap <= 128 ? MB_SENSOR_BLOCKS 
                 const uint32_t kv = kvs[t];
                 const float oz = __uint_as_float(kv & ~kOrderMask);
                 const uint32_t order = kv & kOrderMask;
-                const bool inner = cls[t] == kWallInner, none = cls[t] == kWallNone;
+                int cls = kWallInner;
+#ifndef MB_PROBE_ALL_DEEP   // (instruction-count probe: wrong rows near the walls)
+                if (!(oin & beats_wall(p.x, p.y, dx, dy, cs[t]))) {
+                    const float sn = R.s[4 * g + t];
+                    const float ex = cs[t] * h.x + sn * h.y, ey = cs[t] * h.y + sn * (-h.x);
+                    cls = wall_class(p.x, p.y, dx, dy, cs[t], fw ? p.x + ex : p.x - ex, fw ? p.y + ey : p.y - ey);
+                }
+#endif
+                const bool inner = cls == kWallInner, none = cls == kWallNone;
                 const bool obj = (kv != kNoKey) & ((inner & beats_wall(p.x, p.y, dx, dy, oz)) | none);
                 // (any index in range: the species is used only for an agent's order)
                 const int spv = (int)L.sp[(order - kOrderAgent) & (kCap - 1)];
                 const int sem = obj ? (order < kOrderAgent ? 6 : spv) : (none ? -1 : 5);
                 semv |= (uint32_t)(uint8_t)(int8_t)sem << (8 * t);
                 if (depth) {
-                    const float z = obj ? oz : inner ? wall_z(p.x, p.y, dx, dy) : none ? __builtin_inff() : s0[t];
+                    const float z = obj ? oz : inner ? wall_z(p.x, p.y, dx, dy) : none ? __builtin_inff() : cs[t];
                     depv |= (uint32_t)depth_u8(z) << (8 * t);
                 }
             }
@@ -1440,23 +1390,17 @@ __global__ __launch_bounds__(64 * kSensorWorlds, kCap <= 128 ? MB_SENSOR_BLOCKS 
             }
         }
         if ((int)lane < nc) {
-            const int i = L.ord[a0 + (int)lane];
+            const int i = a0 + (int)lane;
             const float2 p = L.obj[nf + i], h = L.hd[i];
             const uint32_t kv = L.key[lane * kKeyStride + kSensor];
             const uint32_t order = kv & kOrderMask;
-            // the centre ray's near point (1.1 ahead): in the inner rectangle
-            // unless the agent is within 1.1 of its edge
-#ifdef MB_PROBE_ALL_DEEP
-            const bool deep = true;
-#else
-            const bool deep = (p.x >= kInLo + 1.2f) & (p.x <= kInHiX - 1.2f) & (p.y >= kInLo + 1.2f) &
-                              (p.y <= kInHiY - 1.2f);
-#endif
+            // the centre ray's near point (1.1 ahead), as the pixels'
+            const float c = R.c[kSensor];
             int cls = kWallInner;
-            if (!deep) {
-                const float c = R.c[kSensor], sn = R.s[kSensor];
+            if (!((int)inside_arena(p.x, p.y) & (int)beats_wall(p.x, p.y, h.x, h.y, c))) {
+                const float sn = R.s[kSensor];
                 const float ex = c * h.x + sn * h.y, ey = c * h.y + sn * (-h.x);
-                cls = wall_class(p.x + ex, p.y + ey);
+                cls = wall_class(p.x, p.y, h.x, h.y, c, p.x + ex, p.y + ey);
             }
             const bool agent = (kv != kNoKey) & (order >= kOrderAgent) &&
                                (cls == kWallInner ? beats_wall(p.x, p.y, h.x, h.y, __uint_as_float(kv & ~kOrderMask))
