@@ -926,14 +926,17 @@ constexpr float kWedge = 1.41421356f * kAgentR + 0.05f;
 constexpr float kUEps = 2e-3f;                // root-interval margin in u
 // food squares lie inside their circumscribed circle, radius sqrt 2 (1.42 with
 // margin): the wedge |l| <= |f| + sqrt(2) 1.42; candidate pixels from the
-// corner slopes when |f| > kFoodFar and r^2 > kFoodFar2 (the square then lies
-// wholly beyond the near sphere, on one side of the camera plane), every ray
-// exactly (the wide list) otherwise; discs likewise when |f| > 1.5 and
-// r^2 > kCircleFar2
+// corner slopes when |f| > kFoodFar (the square then lies wholly beyond the
+// near sphere, on one side of the camera plane), every ray exactly (the wide
+// list) otherwise; discs likewise beyond kCircleFar
 constexpr float kWedgeFood = 1.41421356f * 1.42f + 0.05f;
-constexpr float kFoodFar = 2.5f;
-constexpr float kFoodFar2 = 6.5f;       // (1.1 + 1.4142)^2 = 6.32: a square wholly beyond the near sphere
-constexpr float kCircleFar2 = 4.2f;     // (1.1 + 0.92)^2 = 4.08: a disc wholly beyond it
+// Far pairs need no near-sphere test: a disc with |f| > 1.5 is met only by
+// rays whose chord midpoint lies >= sqrt(1.5^2 - 0.92^2) = 1.18 > 1.1 along
+// them (so they leave it past the near sphere, and a near point inside it is
+// on such a ray); every point of a square with |f| > 2.55 lies >= 2.55 -
+// 1.4142 = 1.136 > 1.1 ahead.  The r2 kernel's split stands.
+constexpr float kFoodFar = 2.55f;
+constexpr float kCircleFar = 1.5f;
 constexpr float kFarCull = 5.0f;               // P1 angular cull from this |f| on
 
 template <int kCap>
@@ -1036,14 +1039,13 @@ __device__ __forceinline__ void run_survivors(LDS &L, const RayTab &R, int nf, i
         pair_fl(L, nf, a0 + ic, j, f, l, order);
         const bool food = j < nf;
         const float r2 = f * f + l * l;
-        if ((fabsf(f) <= (food ? kFoodFar : 1.5f)) | (r2 <= (food ? kFoodFar2 : kCircleFar2))) {
+        if (fabsf(f) <= (food ? kFoodFar : kCircleFar)) {
             wide = true;
         } else {
-            // A far pair: the object lies wholly beyond the near sphere
-            // (circle: r > 2.02 = 1.1 + 0.92; square: r > 2.55 > 1.1 + its
-            // half-diagonal 1.4142) and on one side of the camera plane
-            // (circle: |f| > 1.5; square: |f| > 2.5, so every corner has
-            // |X| >= 1.08).  Its hit interval in u, approximately: the circle's
+            // A far pair: the object lies on one side of the camera plane and
+            // the near sphere clips none of its rays (circle: |f| > 1.5;
+            // square: |f| > 2.55, so every corner has |X| >= 1.13; see
+            // kFoodFar).  Its hit interval in u, approximately: the circle's
             // roots (lf -+ R sqrt(r^2 - R^2)) / (f^2 - R^2), or the square's
             // extreme corner slopes Y / X.
             const bool fwd = f > 0.0f;
@@ -1082,7 +1084,7 @@ __device__ __forceinline__ void run_survivors(LDS &L, const RayTab &R, int nf, i
             // u) inside the true interval, where the approximate bounds are off
             // by ~1e-6: for a circle the float q(u) is then off by < 1e-4 of a
             // value <= -0.08; for a square every corner's S = Y - u X is
-            // >= 1.08 x 0.08 from 0 (|X| >= 1.08), against a float error of the
+            // >= 1.13 x 0.08 from 0 (|X| >= 1.13), against a float error of the
             // line test < 1e-4.  They are hits carrying the object's key (a far
             // object lies beyond the near sphere: nothing of it is clipped).
             const int kl = k0 + max(c - 1, 0);
@@ -1348,14 +1350,29 @@ __global__ __launch_bounds__(64 * kSensorWorlds, kCap <= 128 ? MB_SENSOR_BLOCKS 
             const float hxs = fw ? h.x : -h.x, hys = fw ? h.y : -h.y;
             const uint32_t kvs[4] = {kv4.x, kv4.y, kv4.z, kv4.w};
             const float us[4] = {u4.x, u4.y, u4.z, u4.w};
-            // each ray's near point P0 = o + c d: from an origin
-            // inside the inner rectangle it lies inside iff the ray's exit lies
-            // beyond view depth c -- the walls' per-axis test at z = c; the rest
-            // (an origin in a wall band, a ray leaving the rectangle within the
-            // near sphere) place P0 itself, a branch few waves take
-            const float4 c4 = *reinterpret_cast<const float4 *>(&R.c[4 * g]);
-            const float cs[4] = {c4.x, c4.y, c4.z, c4.w};
-            const bool oin = inside_arena(p.x, p.y);
+            // an agent 1.2 inside the inner rectangle has every ray's near point
+            // (1.1 from it) in the rectangle: the wall is the exit from it.  The
+            // others place each near point: inner / in a wall box / beyond.
+#ifdef MB_PROBE_ALL_DEEP   // (instruction-count probe: wrong rows near the walls)
+            const bool deep = true;
+#else
+            const bool deep = (p.x >= kInLo + 1.2f) & (p.x <= kInHiX - 1.2f) & (p.y >= kInLo + 1.2f) &
+                              (p.y <= kInHiY - 1.2f);
+#endif
+            // (one branch per lane: the wall class of its four near points)
+            int cls[4] = {kWallInner, kWallInner, kWallInner, kWallInner};
+            float s0[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+            if (!deep) {
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    const int k = 4 * g + t;
+                    const float c = R.c[k], sn = R.s[k];
+                    const float ex = c * h.x + sn * h.y, ey = c * h.y + sn * (-h.x);
+                    const float px = fw ? p.x + ex : p.x - ex, py = fw ? p.y + ey : p.y - ey;
+                    if (!inside_arena(px, py)) cls[t] = in_wall_box(px, py) ? kWallBox : kWallNone;
+                    s0[t] = c;
+                }
+            }
             uint32_t semv = 0, depv = 0;
 #pragma unroll
             for (int t = 0; t < 4; ++t) {
@@ -1364,22 +1381,14 @@ __global__ __launch_bounds__(64 * kSensorWorlds, kCap <= 128 ? MB_SENSOR_BLOCKS 
                 const uint32_t kv = kvs[t];
                 const float oz = __uint_as_float(kv & ~kOrderMask);
                 const uint32_t order = kv & kOrderMask;
-                int cls = kWallInner;
-#ifndef MB_PROBE_ALL_DEEP   // (instruction-count probe: wrong rows near the walls)
-                if (!(oin & beats_wall(p.x, p.y, dx, dy, cs[t]))) {
-                    const float sn = R.s[4 * g + t];
-                    const float ex = cs[t] * h.x + sn * h.y, ey = cs[t] * h.y + sn * (-h.x);
-                    cls = wall_class(p.x, p.y, dx, dy, cs[t], fw ? p.x + ex : p.x - ex, fw ? p.y + ey : p.y - ey);
-                }
-#endif
-                const bool inner = cls == kWallInner, none = cls == kWallNone;
+                const bool inner = cls[t] == kWallInner, none = cls[t] == kWallNone;
                 const bool obj = (kv != kNoKey) & ((inner & beats_wall(p.x, p.y, dx, dy, oz)) | none);
                 // (any index in range: the species is used only for an agent's order)
                 const int spv = (int)L.sp[(order - kOrderAgent) & (kCap - 1)];
                 const int sem = obj ? (order < kOrderAgent ? 6 : spv) : (none ? -1 : 5);
                 semv |= (uint32_t)(uint8_t)(int8_t)sem << (8 * t);
                 if (depth) {
-                    const float z = obj ? oz : inner ? wall_z(p.x, p.y, dx, dy) : none ? __builtin_inff() : cs[t];
+                    const float z = obj ? oz : inner ? wall_z(p.x, p.y, dx, dy) : none ? __builtin_inff() : s0[t];
                     depv |= (uint32_t)depth_u8(z) << (8 * t);
                 }
             }
@@ -1394,13 +1403,19 @@ __global__ __launch_bounds__(64 * kSensorWorlds, kCap <= 128 ? MB_SENSOR_BLOCKS 
             const float2 p = L.obj[nf + i], h = L.hd[i];
             const uint32_t kv = L.key[lane * kKeyStride + kSensor];
             const uint32_t order = kv & kOrderMask;
-            // the centre ray's near point (1.1 ahead), as the pixels'
-            const float c = R.c[kSensor];
+            // the centre ray's near point (1.1 ahead): in the inner rectangle
+            // unless the agent is within 1.1 of its edge
+#ifdef MB_PROBE_ALL_DEEP
+            const bool deep = true;
+#else
+            const bool deep = (p.x >= kInLo + 1.2f) & (p.x <= kInHiX - 1.2f) & (p.y >= kInLo + 1.2f) &
+                              (p.y <= kInHiY - 1.2f);
+#endif
             int cls = kWallInner;
-            if (!((int)inside_arena(p.x, p.y) & (int)beats_wall(p.x, p.y, h.x, h.y, c))) {
-                const float sn = R.s[kSensor];
+            if (!deep) {
+                const float c = R.c[kSensor], sn = R.s[kSensor];
                 const float ex = c * h.x + sn * h.y, ey = c * h.y + sn * (-h.x);
-                cls = wall_class(p.x, p.y, h.x, h.y, c, p.x + ex, p.y + ey);
+                cls = wall_class(p.x + ex, p.y + ey);
             }
             const bool agent = (kv != kNoKey) & (order >= kOrderAgent) &&
                                (cls == kWallInner ? beats_wall(p.x, p.y, h.x, h.y, __uint_as_float(kv & ~kOrderMask))

@@ -1,0 +1,25 @@
+#!/usr/bin/env python3
+"""Counting-probe builds (build_var/probe_*.so: the sensor adds a per-world
+counter into the overflow column): counter total / (worlds x steps)."""
+import glob, os, subprocess, sys, json
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+code = r'''
+import sys, json; sys.path.insert(0, "madrona-bots_amd")
+import torch, madrona_bots as mb
+W = 65536
+m = mb.SimManager(0, W, 69, 32)
+m.write_synthetic_actions(1234, 0)
+for t in range(200):
+    m.step(); m.shift_observations(); m.write_synthetic_actions(1234, t + 1)
+torch.cuda.synchronize()
+a = m.overflow()
+n0 = m.agent_steps()
+for t in range(200, 220):
+    m.step(); m.shift_observations(); m.write_synthetic_actions(1234, t + 1)
+torch.cuda.synchronize()
+print(json.dumps({"per_world_step": (m.overflow() - a) / (W * 20), "agents_per_world": (m.agent_steps() - n0) / (W * 20)}))
+'''
+for lib in sorted(glob.glob(os.path.join(ROOT, "build_var", "probe_*.so"))):
+    env = dict(os.environ, MBOTS_LIB=lib)
+    r = subprocess.run([sys.executable, "-c", code], env=env, cwd=ROOT, capture_output=True, text=True, timeout=120)
+    print(os.path.basename(lib), r.stdout.strip() or r.stderr[-300:], flush=True)
