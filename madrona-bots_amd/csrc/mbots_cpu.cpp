@@ -530,9 +530,9 @@ void Sim::sensor_world(uint32_t w, Table &nxt)
         }
         // each ray's near point: in the inner rectangle (the wall is the exit
         // from it), inside a wall box (the wall, at s0) or beyond (a miss)
-        auto cls_of = [&](int k, bool fwd, float dx, float dy) {
+        auto cls_of = [&](int k, bool fwd) {
             const float ex = np[k].c * h.x + np[k].s * h.y, ey = np[k].c * h.y + np[k].s * (-h.x);
-            return wall_class(ax, ay, dx, dy, np[k].c, fwd ? ax + ex : ax - ex, fwd ? ay + ey : ay - ey);
+            return wall_class(fwd ? ax + ex : ax - ex, fwd ? ay + ey : ay - ey);
         };
         const size_t r = (size_t)obsrow_[base + i];
         for (int k = 0; k < kSensor; ++k) {
@@ -542,7 +542,7 @@ void Sim::sensor_world(uint32_t w, Table &nxt)
             const uint32_t kv = key[k];
             const float oz = u2f(kv & ~kOrderMask);
             const uint32_t order = kv & kOrderMask;
-            const int cls = cls_of(k, fwd, dx, dy);
+            const int cls = cls_of(k, fwd);
             const bool obj = (kv != kNoKey) && (cls == kWallInner ? beats_wall(ax, ay, dx, dy, oz) : cls == kWallNone);
             nxt.sem[r * kSensor + k] = (int8_t)(obj ? (order < kOrderAgent ? 6 : species_[base + order - kOrderAgent])
                                                     : (cls == kWallNone ? -1 : 5));
@@ -552,7 +552,7 @@ void Sim::sensor_world(uint32_t w, Table &nxt)
                                                       : cls == kWallBox ? np[k].c : __builtin_inff());
         }
         const uint32_t kv = key[kSensor], order = kv & kOrderMask;
-        const int fcls = cls_of(kSensor, true, h.x, h.y);
+        const int fcls = cls_of(kSensor, true);
         const bool agent = kv != kNoKey && order >= kOrderAgent &&
                            (fcls == kWallInner ? beats_wall(ax, ay, h.x, h.y, u2f(kv & ~kOrderMask)) : fcls == kWallNone);
         finder_[base + i] = agent ? (int32_t)(order - kOrderAgent) : -1;

@@ -1359,24 +1359,18 @@ __global__ __launch_bounds__(64 * kSensorWorlds, kCap <= 128 ? MB_SENSOR_BLOCKS 
             const bool deep = (p.x >= kInLo + 1.2f) & (p.x <= kInHiX - 1.2f) & (p.y >= kInLo + 1.2f) &
                               (p.y <= kInHiY - 1.2f);
 #endif
-            // (one branch per lane: the wall class of its four near points
-            // P0 = o + c d -- from an origin inside the inner rectangle P0 is
-            // inside iff the ray's exit lies beyond view depth c, the walls'
-            // per-axis test at z = c; otherwise P0 is placed itself)
+            // (one branch per lane: the wall class of its four near points)
             int cls[4] = {kWallInner, kWallInner, kWallInner, kWallInner};
-            const float4 c4 = *reinterpret_cast<const float4 *>(&R.c[4 * g]);
-            const float s0[4] = {c4.x, c4.y, c4.z, c4.w};
+            float s0[4] = {0.0f, 0.0f, 0.0f, 0.0f};
             if (!deep) {
-                const bool oin = inside_arena(p.x, p.y);
 #pragma unroll
                 for (int t = 0; t < 4; ++t) {
-                    const float dx = hxs + us[t] * hys, dy = hys + us[t] * (-hxs);
-                    if (!((int)oin & (int)beats_wall(p.x, p.y, dx, dy, s0[t]))) {
-                        const float sn = R.s[4 * g + t];
-                        const float ex = s0[t] * h.x + sn * h.y, ey = s0[t] * h.y + sn * (-h.x);
-                        cls[t] = wall_class(p.x, p.y, dx, dy, s0[t], fw ? p.x + ex : p.x - ex,
-                                            fw ? p.y + ey : p.y - ey);
-                    }
+                    const int k = 4 * g + t;
+                    const float c = R.c[k], sn = R.s[k];
+                    const float ex = c * h.x + sn * h.y, ey = c * h.y + sn * (-h.x);
+                    const float px = fw ? p.x + ex : p.x - ex, py = fw ? p.y + ey : p.y - ey;
+                    if (!inside_arena(px, py)) cls[t] = in_wall_box(px, py) ? kWallBox : kWallNone;
+                    s0[t] = c;
                 }
             }
             uint32_t semv = 0, depv = 0;
@@ -1421,7 +1415,7 @@ __global__ __launch_bounds__(64 * kSensorWorlds, kCap <= 128 ? MB_SENSOR_BLOCKS 
             if (!deep) {
                 const float c = R.c[kSensor], sn = R.s[kSensor];
                 const float ex = c * h.x + sn * h.y, ey = c * h.y + sn * (-h.x);
-                cls = wall_class(p.x, p.y, h.x, h.y, c, p.x + ex, p.y + ey);
+                cls = wall_class(p.x + ex, p.y + ey);
             }
             const bool agent = (kv != kNoKey) & (order >= kOrderAgent) &&
                                (cls == kWallInner ? beats_wall(p.x, p.y, h.x, h.y, __uint_as_float(kv & ~kOrderMask))

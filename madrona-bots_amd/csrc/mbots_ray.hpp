@@ -91,16 +91,12 @@ MB_HD bool beats_wall(float ox, float oy, float dx, float dy, float z)
     return bx & by;
 }
 
-// where a ray's near point P0 = o + c d lies: the inner rectangle (the wall is
-// the exit from it), inside a wall box (the wall, at s0), or beyond the walls
-// (a miss).  From an origin inside the inner rectangle P0 lies inside iff the
-// ray's exit lies beyond view depth c -- beats_wall at z = c (strict); from an
-// origin in a wall band, by P0's coordinates (the oracle's resolve)
+// where a ray's near point P0 lies: the inner rectangle (the wall is the exit
+// from it), inside a wall box (the wall, at s0), or beyond the walls (a miss)
 constexpr int kWallInner = 0, kWallBox = 1, kWallNone = 2;
-MB_HD int wall_class(float ox, float oy, float dx, float dy, float c, float px, float py)
+MB_HD int wall_class(float px, float py)
 {
-    const bool inner = inside_arena(ox, oy) ? beats_wall(ox, oy, dx, dy, c) : inside_arena(px, py);
-    return inner ? kWallInner : in_wall_box(px, py) ? kWallBox : kWallNone;
+    return inside_arena(px, py) ? kWallInner : in_wall_box(px, py) ? kWallBox : kWallNone;
 }
 
 MB_HD uint32_t order_of(int nf, int j)

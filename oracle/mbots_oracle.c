@@ -782,12 +782,7 @@ static orc_hit resolve(orc_hit h, int k, float ox, float oy, float hx, float hy)
     float px = fwd ? ox + ex : ox - ex, py = fwd ? oy + ey : oy - ey;
     int obj = h.order != 0xFFFFFFFFu;
     orc_hit out = h;
-    /* P0 = o + c d: from an origin inside the inner rectangle it lies inside
-     * iff the ray's exit from the rectangle lies beyond view depth c -- the
-     * walls' per-axis test at z = c (strict); from an origin in a wall band,
-     * by its coordinates */
-    int inner = in_inner(ox, oy) ? beats_wall(ox, oy, dx, dy, c) : in_inner(px, py);
-    if (inner) {
+    if (in_inner(px, py)) {
         if (!obj || !beats_wall(ox, oy, dx, dy, h.z)) { out.z = wall_z(ox, oy, dx, dy); out.order = 0; }
     } else if (in_wall_box(px, py)) {
         out.z = c;
