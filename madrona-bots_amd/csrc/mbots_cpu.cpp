@@ -53,71 +53,22 @@ void Table::resize(size_t rows)
     put(depth, rows * kSensor); put(pdepth, rows * kSensor);
 }
 
-Pool::~Pool()
-{
-    {
-        std::lock_guard<std::mutex> lk(m_);
-        stop_ = true;
-    }
-    go_.notify_all();
-    for (auto &t : th_) t.join();
-}
-
-void Pool::start()
-{
-    for (unsigned t = 1; t < T_; ++t) th_.emplace_back([this] { work(); });
-}
-
-void Pool::work()
-{
-    uint64_t seen = 0;
-    for (;;) {
-        const std::function<void(uint32_t)> *fn;
-        uint32_t n, chunk;
-        {
-            std::unique_lock<std::mutex> lk(m_);
-            go_.wait(lk, [&] { return stop_ || gen_ != seen; });
-            if (stop_) return;
-            seen = gen_;
-            fn = fn_;
-            n = n_;
-            chunk = chunk_;
-        }
-        for (uint32_t lo; (lo = next_.fetch_add(chunk)) < n;)
-            for (uint32_t w = lo, hi = std::min(n, lo + chunk); w < hi; ++w) (*fn)(w);
-        std::lock_guard<std::mutex> lk(m_);
-        if (--busy_ == 0) done_.notify_one();
-    }
-}
-
-void Pool::run(uint32_t n, const std::function<void(uint32_t)> &fn)
-{
-    if (T_ <= 1 || n <= 1) {
-        for (uint32_t w = 0; w < n; ++w) fn(w);
-        return;
-    }
-    if (th_.empty()) start();
-    const uint32_t chunk = std::max<uint32_t>(1u, n / (8u * T_));
-    {
-        std::lock_guard<std::mutex> lk(m_);
-        fn_ = &fn;
-        n_ = n;
-        chunk_ = chunk;
-        next_.store(0);
-        busy_ = (unsigned)th_.size();
-        ++gen_;
-    }
-    go_.notify_all();
-    for (uint32_t lo; (lo = next_.fetch_add(chunk)) < n;)
-        for (uint32_t w = lo, hi = std::min(n, lo + chunk); w < hi; ++w) fn(w);
-    std::unique_lock<std::mutex> lk(m_);
-    done_.wait(lk, [&] { return busy_ == 0; });
-}
-
 template <typename F> void Sim::for_worlds(F &&fn) const
 {
-    const std::function<void(uint32_t)> f(std::forward<F>(fn));
-    pool_->run(W_, f);
+    const unsigned T = std::max(1u, std::min<unsigned>(threads_, W_));
+    if (T == 1) {
+        for (uint32_t w = 0; w < W_; ++w) fn(w);
+        return;
+    }
+    std::vector<std::thread> th;
+    th.reserve(T);
+    for (unsigned t = 0; t < T; ++t) {
+        const uint32_t lo = (uint32_t)((uint64_t)W_ * t / T), hi = (uint32_t)((uint64_t)W_ * (t + 1) / T);
+        th.emplace_back([&fn, lo, hi] {
+            for (uint32_t w = lo; w < hi; ++w) fn(w);
+        });
+    }
+    for (auto &t : th) t.join();
 }
 
 Sim::Sim(const mbots_config &cfg)
@@ -126,10 +77,11 @@ Sim::Sim(const mbots_config &cfg)
 {
     const char *e = getenv("MBOTS_CPU_THREADS");
     // default: the machine's threads up to 16 (a GPU box's per-GPU CPU share;
-    // MBOTS_CPU_THREADS overrides, e.g. bench.py's all-core baseline)
+    // MBOTS_CPU_THREADS overrides, e.g. bench.py's all-core baseline).  Each
+    // phase starts its threads on contiguous world ranges: a persistent pool
+    // with dynamic chunks measured 2x slower on the GPU box (16-CPU cgroup)
     threads_ = e ? (unsigned)atoi(e) : std::min(16u, std::thread::hardware_concurrency());
     if (threads_ == 0) threads_ = 1;
-    pool_ = std::make_unique<Pool>(threads_);
     const size_t rows = (size_t)W_ * cap_;
     for (auto *v : {&x_, &y_, &rw_, &rz_, &sur0_, &sur1_}) put(*v, rows);
     for (auto *v : {&species_, &health_, &finder_, &obsrow_}) put(*v, rows);

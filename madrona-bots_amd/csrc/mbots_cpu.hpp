@@ -12,14 +12,8 @@
 #include "../../include/mbots.h"
 #include "mbots_device.hpp"
 
-#include <atomic>
-#include <condition_variable>
 #include <cstdint>
-#include <functional>
-#include <memory>
-#include <mutex>
 #include <string>
-#include <thread>
 #include <vector>
 
 namespace mbots {
@@ -32,30 +26,6 @@ struct Table {
     std::vector<int8_t> sem, psem;
     std::vector<uint8_t> depth, pdepth;
     void resize(size_t rows);
-};
-
-// Persistent worker threads for the world-parallel phases (created on first
-// use, joined with the Sim): a phase hands out chunks of worlds through an
-// atomic cursor, the calling thread working alongside the workers
-class Pool {
-public:
-    explicit Pool(unsigned threads) : T_(threads) {}
-    ~Pool();
-    void run(uint32_t n, const std::function<void(uint32_t)> &fn);
-
-private:
-    void work();
-    void start();
-    unsigned T_;
-    std::vector<std::thread> th_;
-    std::mutex m_;
-    std::condition_variable go_, done_;
-    const std::function<void(uint32_t)> *fn_ = nullptr;
-    uint32_t n_ = 0, chunk_ = 1;
-    std::atomic<uint32_t> next_{0};
-    unsigned busy_ = 0;
-    uint64_t gen_ = 0;
-    bool stop_ = false;
 };
 
 class Sim {
@@ -91,7 +61,6 @@ private:
     mbots_config cfg_;
     uint32_t W_, Wx_, cap_, A_;   // simulated / exported worlds (W_ = Wx_ + the shard ghost)
     unsigned threads_;
-    std::unique_ptr<Pool> pool_;   // (mutable through the pointer: for_worlds is const)
     // agent state, [W][cap] (slot order = creation order, survivors compacted)
     std::vector<float> x_, y_, rw_, rz_, sur0_, sur1_;
     std::vector<int32_t> species_, health_, finder_, obsrow_;
