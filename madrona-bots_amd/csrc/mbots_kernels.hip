@@ -1350,29 +1350,9 @@ __global__ __launch_bounds__(64 * kSensorWorlds, kCap <= 128 ? MB_SENSOR_BLOCKS 
             const float hxs = fw ? h.x : -h.x, hys = fw ? h.y : -h.y;
             const uint32_t kvs[4] = {kv4.x, kv4.y, kv4.z, kv4.w};
             const float us[4] = {u4.x, u4.y, u4.z, u4.w};
-            // an agent 1.2 inside the inner rectangle has every ray's near point
-            // (1.1 from it) in the rectangle: the wall is the exit from it.  The
-            // others place each near point: inner / in a wall box / beyond.
-#ifdef MB_PROBE_ALL_DEEP   // (instruction-count probe: wrong rows near the walls)
-            const bool deep = true;
-#else
-            const bool deep = (p.x >= kInLo + 1.2f) & (p.x <= kInHiX - 1.2f) & (p.y >= kInLo + 1.2f) &
-                              (p.y <= kInHiY - 1.2f);
-#endif
-            // (one branch per lane: the wall class of its four near points)
-            int cls[4] = {kWallInner, kWallInner, kWallInner, kWallInner};
-            float s0[4] = {0.0f, 0.0f, 0.0f, 0.0f};
-            if (!deep) {
-#pragma unroll
-                for (int t = 0; t < 4; ++t) {
-                    const int k = 4 * g + t;
-                    const float c = R.c[k], sn = R.s[k];
-                    const float ex = c * h.x + sn * h.y, ey = c * h.y + sn * (-h.x);
-                    const float px = fw ? p.x + ex : p.x - ex, py = fw ? p.y + ey : p.y - ey;
-                    if (!inside_arena(px, py)) cls[t] = in_wall_box(px, py) ? kWallBox : kWallNone;
-                    s0[t] = c;
-                }
-            }
+            // every ray as if its near point lay in the inner rectangle (true
+            // for every agent 1.2 inside it: the wall is the ray's exit); the
+            // rays of the others are redone below
             uint32_t semv = 0, depv = 0;
 #pragma unroll
             for (int t = 0; t < 4; ++t) {
@@ -1381,14 +1361,13 @@ __global__ __launch_bounds__(64 * kSensorWorlds, kCap <= 128 ? MB_SENSOR_BLOCKS 
                 const uint32_t kv = kvs[t];
                 const float oz = __uint_as_float(kv & ~kOrderMask);
                 const uint32_t order = kv & kOrderMask;
-                const bool inner = cls[t] == kWallInner, none = cls[t] == kWallNone;
-                const bool obj = (kv != kNoKey) & ((inner & beats_wall(p.x, p.y, dx, dy, oz)) | none);
+                const bool obj = (kv != kNoKey) & beats_wall(p.x, p.y, dx, dy, oz);
                 // (any index in range: the species is used only for an agent's order)
                 const int spv = (int)L.sp[(order - kOrderAgent) & (kCap - 1)];
-                const int sem = obj ? (order < kOrderAgent ? 6 : spv) : (none ? -1 : 5);
+                const int sem = obj ? (order < kOrderAgent ? 6 : spv) : 5;
                 semv |= (uint32_t)(uint8_t)(int8_t)sem << (8 * t);
                 if (depth) {
-                    const float z = obj ? oz : inner ? wall_z(p.x, p.y, dx, dy) : none ? __builtin_inff() : s0[t];
+                    const float z = obj ? oz : wall_z(p.x, p.y, dx, dy);
                     depv |= (uint32_t)depth_u8(z) << (8 * t);
                 }
             }
@@ -1398,29 +1377,69 @@ __global__ __launch_bounds__(64 * kSensorWorlds, kCap <= 128 ? MB_SENSOR_BLOCKS 
                 if (depth) st_stream(reinterpret_cast<uint32_t *>(nxt.depth + (size_t)r * kSensor) + g, depv, nt);
             }
         }
+        bool shallow = false;   // lane a < nc: agent a0 + a is within 1.2 of the inner rectangle's edge
         if ((int)lane < nc) {
             const int i = a0 + (int)lane;
             const float2 p = L.obj[nf + i], h = L.hd[i];
             const uint32_t kv = L.key[lane * kKeyStride + kSensor];
             const uint32_t order = kv & kOrderMask;
-            // the centre ray's near point (1.1 ahead): in the inner rectangle
-            // unless the agent is within 1.1 of its edge
-#ifdef MB_PROBE_ALL_DEEP
-            const bool deep = true;
-#else
-            const bool deep = (p.x >= kInLo + 1.2f) & (p.x <= kInHiX - 1.2f) & (p.y >= kInLo + 1.2f) &
-                              (p.y <= kInHiY - 1.2f);
+#ifndef MB_PROBE_ALL_DEEP   // (instruction-count probe: wrong rows near the walls)
+            shallow = !((p.x >= kInLo + 1.2f) & (p.x <= kInHiX - 1.2f) & (p.y >= kInLo + 1.2f) &
+                        (p.y <= kInHiY - 1.2f));
 #endif
-            int cls = kWallInner;
-            if (!deep) {
-                const float c = R.c[kSensor], sn = R.s[kSensor];
-                const float ex = c * h.x + sn * h.y, ey = c * h.y + sn * (-h.x);
-                cls = wall_class(p.x + ex, p.y + ey);
-            }
             const bool agent = (kv != kNoKey) & (order >= kOrderAgent) &&
-                               (cls == kWallInner ? beats_wall(p.x, p.y, h.x, h.y, __uint_as_float(kv & ~kOrderMask))
-                                                  : cls == kWallNone);
+                               beats_wall(p.x, p.y, h.x, h.y, __uint_as_float(kv & ~kOrderMask));
             S.finder[base + i] = agent ? (int32_t)(order - kOrderAgent) : -1;
+        }
+        // ---- the agents near the walls: each ray's near point
+        // P0 = o + c d placed -- in the inner rectangle (the pass above stands),
+        // inside a wall box (the wall at view depth c: objects hidden) or beyond
+        // the walls (a miss: semantic -1, objects seen); two agents per
+        // iteration, lane = (agent, ray), the finder ray on lane 0 of each half
+        uint64_t sm = ballot64(shallow);
+        while (sm != 0ull) {   // wave-uniform
+            const int a_lo = (int)__builtin_ctzll(sm);
+            sm &= sm - 1ull;
+            const int a_hi = sm != 0ull ? (int)__builtin_ctzll(sm) : -1;
+            if (sm != 0ull) sm &= sm - 1ull;
+            const int ca = lane < 32 ? a_lo : a_hi;
+            const int i = a0 + max(ca, 0);
+            int r = __shfl(rows[0], i & 63);
+#pragma unroll
+            for (int gg = 1; gg < kG; ++gg) {
+                const int rg = __shfl(rows[gg], i & 63);
+                if ((i >> 6) == gg) r = rg;
+            }
+            if (ca >= 0) {
+                const int k = (int)(lane & 31u);
+                const float2 p = L.obj[nf + i], h = L.hd[i];
+                const bool fw = k < 24;
+                const float c = R.c[k], sn = R.s[k];
+                const float ex = c * h.x + sn * h.y, ey = c * h.y + sn * (-h.x);
+                const int cls = wall_class(fw ? p.x + ex : p.x - ex, fw ? p.y + ey : p.y - ey);
+                if (cls != kWallInner) {
+                    const uint32_t kv = L.key[ca * kKeyStride + k];
+                    const float oz = __uint_as_float(kv & ~kOrderMask);
+                    const uint32_t order = kv & kOrderMask;
+                    const bool none = cls == kWallNone;
+                    const bool obj = (kv != kNoKey) & none;
+                    const int spv = (int)L.sp[(order - kOrderAgent) & (kCap - 1)];
+                    const int sem = obj ? (order < kOrderAgent ? 6 : spv) : (none ? -1 : 5);
+                    nxt.sem[(size_t)r * kSensor + k] = (int8_t)sem;
+                    if (depth) nxt.depth[(size_t)r * kSensor + k] = depth_u8(obj ? oz : none ? __builtin_inff() : c);
+                }
+                if (k == 0) {   // the finder ray (u = 0, near point 1.1 ahead)
+                    const float fc = R.c[kSensor], fsn = R.s[kSensor];
+                    const float fx = fc * h.x + fsn * h.y, fy = fc * h.y + fsn * (-h.x);
+                    const int fcls = wall_class(p.x + fx, p.y + fy);
+                    if (fcls != kWallInner) {
+                        const uint32_t kv = L.key[ca * kKeyStride + kSensor];
+                        const uint32_t order = kv & kOrderMask;
+                        const bool agent = (kv != kNoKey) & (order >= kOrderAgent) & (fcls == kWallNone);
+                        S.finder[base + i] = agent ? (int32_t)(order - kOrderAgent) : -1;
+                    }
+                }
+            }
         }
 #endif
         wave_sync();
