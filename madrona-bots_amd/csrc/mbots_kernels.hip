@@ -921,15 +921,14 @@ __global__ __launch_bounds__(256) void shift_move_kernel(const uint32_t *totals,
 constexpr int kKeyAgents = MB_KEY_AGENTS;     // agents per chunk (key rows)
 constexpr int kKeyStride = 36;                // key row: 32 pixels, finder, pad (16-B rows)
 constexpr int kQueueCap = 128;                // P1 survivors (flushed at >= 64)
-// |l| <= |f| + R sqrt(2): necessary for a radius-R disc on a ray |u| < 1
-constexpr float kWedge = 1.41421356f * kAgentR + 0.05f;
+// P1's wedge |l| <= |f| + R sqrt(2) + 0.05 is necessary for a radius-R disc
+// (a food square: its circumscribed circle, R = 1.42) on a ray |u| < 1
 constexpr float kUEps = 2e-3f;                // root-interval margin in u
 // food squares lie inside their circumscribed circle, radius sqrt 2 (1.42 with
 // margin): the wedge |l| <= |f| + sqrt(2) 1.42; candidate pixels from the
 // corner slopes when |f| > kFoodFar (the square then lies wholly beyond the
 // near sphere, on one side of the camera plane), every ray exactly (the wide
 // list) otherwise; discs likewise beyond kCircleFar
-constexpr float kWedgeFood = 1.41421356f * 1.42f + 0.05f;
 // Far pairs need no near-sphere test: a disc with |f| > 1.5 is met only by
 // rays whose chord midpoint lies >= sqrt(1.5^2 - 0.92^2) = 1.18 > 1.1 along
 // them (so they leave it past the near sphere, and a near point inside it is
@@ -990,9 +989,18 @@ __device__ __forceinline__ void pair_fl(const LDS &L, int nf, int i, int j, floa
 
 // W: wide pairs qcode[q0, q0 + cnt), two per wave (32 lanes each: rays 0..31,
 // lane 0 of each half also takes the finder ray)
+// (MB_COUNT = k: counting-probe builds, scripts/probe_counts.py; event k's
+// wave-uniform count summed into the overflow column)
+#ifdef MB_COUNT
+#define MB_CNT(k, v) do { if (MB_COUNT == (k)) mbc += (uint32_t)(v); } while (0)
+#else
+#define MB_CNT(k, v) do { } while (0)
+#endif
+
 template <class LDS>
-__device__ __forceinline__ void run_wide(LDS &L, const RayTab &R, int nf, int a0, int q0, int cnt)
+__device__ __forceinline__ void run_wide(LDS &L, const RayTab &R, int nf, int a0, int q0, int cnt, uint32_t &mbc)
 {
+    MB_CNT(6, (cnt + 1) / 2);
     const int lane = (int)__lane_id();
     // ray k's offset and near point (the near sphere): loop invariant
     const int k = lane & 31;
@@ -1026,8 +1034,14 @@ __device__ __forceinline__ void run_wide(LDS &L, const RayTab &R, int nf, int a0
 // candidate pixels; the edge pixels and the finder get the exact test inline,
 // near pairs go to the wide list
 template <class LDS>
-__device__ __forceinline__ void run_survivors(LDS &L, const RayTab &R, int nf, int a0, int q0, int cnt)
+__device__ __forceinline__ void run_survivors(LDS &L, const RayTab &R, int nf, int a0, int q0, int cnt, uint32_t &mbc)
 {
+    MB_CNT(3, 1);
+    MB_CNT(4, cnt);
+#ifdef MB_COUNT
+    int mb_t = 0;
+    bool mb_food = false;
+#endif
     const int lane = (int)__lane_id();
     bool wide = false;
     uint32_t code = 0;
@@ -1107,16 +1121,26 @@ __device__ __forceinline__ void run_survivors(LDS &L, const RayTab &R, int nf, i
             if ((c > 1) & hb) atomicMin(&kr[kl], kin);
             if (hf) atomicMin(&kr[kSensor], kin);
             for (int k = k0 + 1; k < kl; ++k) atomicMin(&kr[k], kin);
+#ifdef MB_COUNT
+            mb_t = max(kl - k0 - 1, 0);
+            mb_food = food;
+#endif
         }
     }
     // every lane read its code above: the wide ones compact in place
     const uint64_t wm = ballot64(wide);
     if (wide) L.qcode[q0 + (int)rank_below(wm)] = code;
     const int nw = __popcll(wm);
+    MB_CNT(5, nw);
+#ifdef MB_COUNT
+    for (int o = 32; o > 0; o >>= 1) mb_t = max(mb_t, __shfl_xor(mb_t, o));
+    MB_CNT(7, mb_t);
+    MB_CNT(9, __popcll(ballot64(mb_food)));
+#endif
 #ifndef MB_SKIP_WIDE   // (instruction-count probes only: MB_SKIP_* builds give wrong rows)
     if (nw > 0) {
         wave_sync();
-        run_wide(L, R, nf, a0, q0, nw);
+        run_wide(L, R, nf, a0, q0, nw, mbc);
         wave_sync();
     }
 #endif
@@ -1250,8 +1274,10 @@ __global__ __launch_bounds__(64 * kSensorWorlds, kCap <= 128 ? MB_SENSOR_BLOCKS 
     if (kPad) L.obj[nobj + (int)lane] = make_float2(__builtin_nanf(""), __builtin_nanf(""));
     wave_sync();
 
+    uint32_t mbc = 0;
     for (int a0 = kChunk0; a0 < n; a0 += kChunkStep) {
         const int nc = min(kKeyAgents, n - a0);
+        MB_CNT(1, 1);
         for (int q = lane; q < nc * kKeyStride; q += 64) L.key[q] = kNoKey;
         wave_sync();
         // ---- P1: wedge pre-cull of the chunk's (agent, object) pairs.  Lane =
@@ -1268,16 +1294,21 @@ __global__ __launch_bounds__(64 * kSensorWorlds, kCap <= 128 ? MB_SENSOR_BLOCKS 
             const float2 ah = L.hd[ia];
             const int self = nf + ia;
             for (int jb = 0; jb < nobj; jb += G) {
+                MB_CNT(2, 1);
                 const int j = jb + o;
                 // (j >= nobj reads a NaN sentinel: keep comes out false)
                 const float2 p = L.obj[kPad ? j : min(j, nobj - 1)];
                 const float vx = p.x - ap.x, vy = p.y - ap.y;
                 // pair_fl's (f, l) up to an FMA rounding: the cull's margin
-                // (kWedge - sqrt 2 = 0.05) dwarfs it; survivors recompute exactly
+                // (the wedge's + 0.05) dwarfs it; survivors recompute exactly
                 const float f = __builtin_fmaf(vx, ah.x, vy * ah.y), l = __builtin_fmaf(vx, ah.y, -(vy * ah.x));
                 const bool food = j < nf;
                 const float af = fabsf(f);
-                bool keep = (kPad | (j < nobj)) & (j != self) & (fabsf(l) <= af + (food ? kWedgeFood : kWedge));
+                // the object's radius with the cull's 1.001 margin (the wedge's
+                // half-width sqrt(2) rk + 0.05 >= sqrt(2) R + 0.05)
+                const float rk = food ? 1.42f * 1.001f : kAgentR * 1.001f;
+                bool keep = (kPad | (j < nobj)) & (j != self) &
+                            (fabsf(l) <= af + __builtin_fmaf(1.41421356f, rk, 0.05f));
                 {
                     // a far pair (|f| >= kFarCull) also needs a pixel centre, or
                     // forward the finder ray u = 0, within w of its centre's
@@ -1292,14 +1323,15 @@ __global__ __launch_bounds__(64 * kSensorWorlds, kCap <= 128 ? MB_SENSOR_BLOCKS 
                     // as a (1 + u_c^2 / 2 + a (|u_c| + 2.9 a)), never smaller where
                     // it is used: 1.2 (1 + u_c^2 / 2 + a |u_c|) <= 2.9 for a <= 0.285
                     // and |u_c| <= 1 + 2.06 / 5 inside the wedge (5 ops, was 8)
-                    const float ar = (food ? 1.42f * 1.001f : kAgentR * 1.001f) * fabsf(rf);
+                    const float ar = rk * fabsf(rf);
                     const float w = __builtin_fmaf(
                         ar, __builtin_fmaf(ar, __builtin_fmaf(2.9f, ar, fabsf(uc)), __builtin_fmaf(0.5f * uc, uc, 1.0f)),
                         1e-4f);
                     const bool fwd = f > 0.0f;
                     const float sc = fwd ? 12.0f : 4.0f;
                     const float s = __builtin_fmaf(uc, sc, sc - 0.5f);
-                    const float sn = __builtin_rintf(fminf(fmaxf(s, 0.0f), fwd ? 23.0f : 7.0f));
+                    // (the last pixel 2 sc - 1: 23 forward, 7 backward)
+                    const float sn = __builtin_rintf(fminf(fmaxf(s, 0.0f), __builtin_fmaf(2.0f, sc, -1.0f)));
                     const bool pix = fabsf(s - sn) <= sc * w;
                     const bool fin = fwd & (fabsf(uc) <= w);
                     keep = keep & ((af < kFarCull) | pix | fin);
@@ -1311,7 +1343,7 @@ __global__ __launch_bounds__(64 * kSensorWorlds, kCap <= 128 ? MB_SENSOR_BLOCKS 
                 if (nq >= 64) {
                     wave_sync();
 #ifndef MB_SKIP_P2
-                    run_survivors(L, R, nf, a0, nq - 64, 64);
+                    run_survivors(L, R, nf, a0, nq - 64, 64, mbc);
 #endif
                     nq -= 64;
                 }
@@ -1320,7 +1352,7 @@ __global__ __launch_bounds__(64 * kSensorWorlds, kCap <= 128 ? MB_SENSOR_BLOCKS 
         if (nq > 0) {
             wave_sync();
 #ifndef MB_SKIP_P2
-            run_survivors(L, R, nf, a0, 0, nq);
+            run_survivors(L, R, nf, a0, 0, nq, mbc);
 #endif
         }
         wave_sync();
@@ -1402,6 +1434,7 @@ __global__ __launch_bounds__(64 * kSensorWorlds, kCap <= 128 ? MB_SENSOR_BLOCKS 
             sm &= sm - 1ull;
             const int a_hi = sm != 0ull ? (int)__builtin_ctzll(sm) : -1;
             if (sm != 0ull) sm &= sm - 1ull;
+            MB_CNT(8, 1);
             const int ca = lane < 32 ? a_lo : a_hi;
             const int i = a0 + max(ca, 0);
             int r = __shfl(rows[0], i & 63);
@@ -1444,6 +1477,11 @@ __global__ __launch_bounds__(64 * kSensorWorlds, kCap <= 128 ? MB_SENSOR_BLOCKS 
 #endif
         wave_sync();
     }
+#ifdef MB_COUNT
+    if (lane == 0) S.overflow[w] += mbc;
+#else
+    (void)mbc;
+#endif
     }
 }
 
