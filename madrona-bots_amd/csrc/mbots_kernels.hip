@@ -1383,8 +1383,10 @@ __global__ __launch_bounds__(64 * kSensorWorlds, kCap <= 128 ? MB_SENSOR_BLOCKS 
             const uint32_t kvs[4] = {kv4.x, kv4.y, kv4.z, kv4.w};
             const float us[4] = {u4.x, u4.y, u4.z, u4.w};
             // every ray as if its near point lay in the inner rectangle (true
-            // for every agent 1.2 inside it: the wall is the ray's exit); the
-            // rays of the others are redone below
+            // for every agent 1.2 inside it: the wall is the ray's exit) and
+            // the agent strictly inside it; the rays of the others are redone
+            // below
+            const float lox = kInLo - p.x, hix = kInHiX - p.x, loy = kInLo - p.y, hiy = kInHiY - p.y;
             uint32_t semv = 0, depv = 0;
 #pragma unroll
             for (int t = 0; t < 4; ++t) {
@@ -1393,7 +1395,7 @@ __global__ __launch_bounds__(64 * kSensorWorlds, kCap <= 128 ? MB_SENSOR_BLOCKS 
                 const uint32_t kv = kvs[t];
                 const float oz = __uint_as_float(kv & ~kOrderMask);
                 const uint32_t order = kv & kOrderMask;
-                const bool obj = (kv != kNoKey) & beats_wall(p.x, p.y, dx, dy, oz);
+                const bool obj = (kv != kNoKey) & beats_wall_in(lox, hix, loy, hiy, dx, dy, oz);
                 // (any index in range: the species is used only for an agent's order)
                 const int spv = (int)L.sp[(order - kOrderAgent) & (kCap - 1)];
                 const int sem = obj ? (order < kOrderAgent ? 6 : spv) : 5;
@@ -1419,15 +1421,19 @@ __global__ __launch_bounds__(64 * kSensorWorlds, kCap <= 128 ? MB_SENSOR_BLOCKS 
             shallow = !((p.x >= kInLo + 1.2f) & (p.x <= kInHiX - 1.2f) & (p.y >= kInLo + 1.2f) &
                         (p.y <= kInHiY - 1.2f));
 #endif
+            // (a shallow agent not strictly inside is redone below)
             const bool agent = (kv != kNoKey) & (order >= kOrderAgent) &&
-                               beats_wall(p.x, p.y, h.x, h.y, __uint_as_float(kv & ~kOrderMask));
+                               beats_wall_in(kInLo - p.x, kInHiX - p.x, kInLo - p.y, kInHiY - p.y, h.x, h.y,
+                                             __uint_as_float(kv & ~kOrderMask));
             S.finder[base + i] = agent ? (int32_t)(order - kOrderAgent) : -1;
         }
         // ---- the agents near the walls: each ray's near point
         // P0 = o + c d placed -- in the inner rectangle (the pass above stands),
         // inside a wall box (the wall at view depth c: objects hidden) or beyond
-        // the walls (a miss: semantic -1, objects seen); two agents per
-        // iteration, lane = (agent, ray), the finder ray on lane 0 of each half
+        // the walls (a miss: semantic -1, objects seen); an agent not strictly
+        // inside the rectangle has its inner rays redone too (beats_wall_in
+        // assumed it); two agents per iteration, lane = (agent, ray), the
+        // finder ray on lane 0 of each half
         uint64_t sm = ballot64(shallow);
         while (sm != 0ull) {   // wave-uniform
             const int a_lo = (int)__builtin_ctzll(sm);
@@ -1450,25 +1456,35 @@ __global__ __launch_bounds__(64 * kSensorWorlds, kCap <= 128 ? MB_SENSOR_BLOCKS 
                 const float c = R.c[k], sn = R.s[k];
                 const float ex = c * h.x + sn * h.y, ey = c * h.y + sn * (-h.x);
                 const int cls = wall_class(fw ? p.x + ex : p.x - ex, fw ? p.y + ey : p.y - ey);
-                if (cls != kWallInner) {
+                const bool edge = !strictly_inside(p.x, p.y);
+                if ((cls != kWallInner) | edge) {
                     const uint32_t kv = L.key[ca * kKeyStride + k];
                     const float oz = __uint_as_float(kv & ~kOrderMask);
                     const uint32_t order = kv & kOrderMask;
-                    const bool none = cls == kWallNone;
-                    const bool obj = (kv != kNoKey) & none;
+                    const bool none = cls == kWallNone, inner = cls == kWallInner;
+                    const float u = R.u[k];
+                    const float hxs = fw ? h.x : -h.x, hys = fw ? h.y : -h.y;
+                    const float dx = hxs + u * hys, dy = hys + u * (-hxs);
+                    const bool obj = (kv != kNoKey) & (none | (inner && beats_wall(p.x, p.y, dx, dy, oz)));
                     const int spv = (int)L.sp[(order - kOrderAgent) & (kCap - 1)];
                     const int sem = obj ? (order < kOrderAgent ? 6 : spv) : (none ? -1 : 5);
                     nxt.sem[(size_t)r * kSensor + k] = (int8_t)sem;
-                    if (depth) nxt.depth[(size_t)r * kSensor + k] = depth_u8(obj ? oz : none ? __builtin_inff() : c);
+                    if (depth) {
+                        const float z = obj ? oz : none ? __builtin_inff() : inner ? wall_z(p.x, p.y, dx, dy) : c;
+                        nxt.depth[(size_t)r * kSensor + k] = depth_u8(z);
+                    }
                 }
                 if (k == 0) {   // the finder ray (u = 0, near point 1.1 ahead)
                     const float fc = R.c[kSensor], fsn = R.s[kSensor];
                     const float fx = fc * h.x + fsn * h.y, fy = fc * h.y + fsn * (-h.x);
                     const int fcls = wall_class(p.x + fx, p.y + fy);
-                    if (fcls != kWallInner) {
+                    if ((fcls != kWallInner) | edge) {
                         const uint32_t kv = L.key[ca * kKeyStride + kSensor];
                         const uint32_t order = kv & kOrderMask;
-                        const bool agent = (kv != kNoKey) & (order >= kOrderAgent) & (fcls == kWallNone);
+                        const bool see = (fcls == kWallNone) |
+                                         ((fcls == kWallInner) &&
+                                          beats_wall(p.x, p.y, h.x, h.y, __uint_as_float(kv & ~kOrderMask)));
+                        const bool agent = (kv != kNoKey) & (order >= kOrderAgent) & see;
                         S.finder[base + i] = agent ? (int32_t)(order - kOrderAgent) : -1;
                     }
                 }

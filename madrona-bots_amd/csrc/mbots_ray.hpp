@@ -91,6 +91,21 @@ MB_HD bool beats_wall(float ox, float oy, float dx, float dy, float z)
     return bx & by;
 }
 
+// beats_wall for an origin strictly inside the inner rectangle (kInLo < o <
+// kInHi on both axes), with lo = kInLo - o and hi = kInHi - o per axis: the
+// same predicate without the sign cases -- for d > 0, lo < 0 <= z d; for d < 0,
+// z d <= 0 < hi; for d == 0 both hold (z d is a signed zero), as beats_wall's
+// d == 0 case; and lo < z d is o - lo > z |d| negated exactly
+MB_HD bool beats_wall_in(float lox, float hix, float loy, float hiy, float dx, float dy, float z)
+{
+    const float zx = z * dx, zy = z * dy;
+    return (lox < zx) & (zx < hix) & (loy < zy) & (zy < hiy);
+}
+MB_HD bool strictly_inside(float ox, float oy)
+{
+    return (ox > kInLo) & (ox < kInHiX) & (oy > kInLo) & (oy < kInHiY);
+}
+
 // where a ray's near point P0 lies: the inner rectangle (the wall is the exit
 // from it), inside a wall box (the wall, at s0), or beyond the walls (a miss)
 constexpr int kWallInner = 0, kWallBox = 1, kWallNone = 2;
