@@ -894,24 +894,30 @@ __global__ __launch_bounds__(256) void shift_move_kernel(const uint32_t *totals,
 // ---------------------------------------------------------------------------
 // K3b sensor: 32-pixel raycast (24 forward + 8 backward) plus the finder ray
 // (Madrona RenderingSystem, sim.cpp:1183-1188).  Build spec:
-// objects are unit circles; in an agent's frame (f along heading h, l along
-// r = (hy, -hx)) ray h + u r meets a circle iff
-//     q(u) = (A u - 2 l f) u + C <= 0,   A = f^2 - 1,  C = l^2 - 1,
-// ahead of the origin iff f + u l > 0 (backward camera: < 0); view depth
-// z = f - 1 (>= 0, 14-bit mantissa).  Per ray the lexicographic minimum of
-// (z, order) over objects (food 1 + k, agents 64 + slot) is seen iff it beats
-// the wall (z * d < X - o per axis), else the wall (order 0).
+// agents are discs of radius R = 0.92, food packages rotated +-1 squares
+// (FoodBox, mbots_ray.hpp); in an agent's frame (f along heading h, l along
+// r = (hy, -hx)) ray h + u r meets a disc iff
+//     q(u) = (A u - 2 l f) u + C <= 0,   A = f^2 - R^2,  C = l^2 - R^2,
+// and sees it iff it leaves it beyond the near sphere (1.1 from the camera:
+// the near point NearPt inside the disc, or the chord's midpoint beyond it);
+// view depth z = f - R (>= 0, 14-bit mantissa).  Per ray the lexicographic
+// minimum of (z, order) over objects (food 1 + k, agents 64 + slot) is seen
+// iff it beats the wall, placed by where the ray's near point lies (inner
+// rectangle: the exit from it; a wall box: the wall at the near point; beyond
+// the walls: no wall, semantic -1).
 //
 // One wave per world, agents in chunks of kKeyAgents; per chunk:
-//  P1  all (agent, object) pairs, one per lane: f, l and the wedge test
-//      |l| <= |f| + sqrt(2) (necessary for any pixel, |u| < 1); survivors and
-//      their (f, l) are ballot-compacted into a queue;
-//  P2  per survivor: approximate roots of q bound its candidate pixels; <= 2
-//      pixels + the finder run the exact predicate inline and ds_min_u32 the
-//      32-bit key (z with its low 9 mantissa bits replaced by the object
-//      order); nearer / wider pairs go to a wide list;
-//  W   wide pairs: two per wave, one lane per ray;
-//  out per (agent, ray): key vs wall -> semantic / depth bytes; finder slot.
+//  P1  all (agent, object) pairs, one per lane: f, l, the wedge test
+//      |l| <= |f| + sqrt(2) R' + 0.05 (necessary for any pixel, |u| < 1) and
+//      for far pairs the angular cull; survivors ballot-compacted into a queue;
+//  P2  per survivor: far pairs (beyond the near sphere's reach) get their hit
+//      interval (disc roots / square corner slopes): the edge pixels and the
+//      finder run the exact predicate, interior pixels are filled, each by
+//      ds_min_u32 of the 32-bit key (z with its low 9 mantissa bits replaced
+//      by the object order); near pairs go to a wide list;
+//  W   wide pairs: two per wave, one lane per ray, every ray exact;
+//  out per (agent, ray): key vs wall -> semantic / depth bytes; finder slot
+//      (every ray as inner first, then a fix-up for the agents near walls).
 // The exact predicate and depths use the same float expressions as
 // oracle/mbots_oracle.c; culling only skips rays it proves cannot pass.
 // ---------------------------------------------------------------------------

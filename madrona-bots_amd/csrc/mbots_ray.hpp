@@ -191,7 +191,7 @@ MB_HD float2 food_cs(uint32_t q22)
 // only (mirrored behind); straddling it, by every ray when the origin is
 // inside (|m1|, |m2| <= 1, the origin in box coordinates), else on the side of
 // the chord, the sign of its slab entry.  Depth (one per object, as the
-// circles' f - 1): the nearest corner's, max(0, f - (|p| + |q|)) forward.
+// discs' f - R): the nearest corner's, max(0, f - (|p| + |q|)) forward.
 struct FoodBox {
     float f, l, p, q, ext;
 };
