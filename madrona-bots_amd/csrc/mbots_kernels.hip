@@ -1530,6 +1530,10 @@ __global__ __launch_bounds__(64 * kSensorWorlds, kCap <= 128 ? MB_SENSOR_BLOCKS 
 // then the block's 64 x 69 contiguous output floats are written coalesced, four
 // per thread as 16-B stores (HBM-bound: 84 B read + 276 B written per row).
 // ---------------------------------------------------------------------------
+#ifndef MB_OBS_NT
+#define MB_OBS_NT 1   // non-temporal stores of the [N, 69] rows (written once, 600 MB at
+                      // 65536 worlds: reference loop -2 % vs plain stores)
+#endif
 constexpr int kObsDim = 69;
 constexpr int kObsRows = 64;
 __global__ __launch_bounds__(256) void construct_obs_kernel(const uint32_t *totals,
@@ -1537,6 +1541,7 @@ __global__ __launch_bounds__(256) void construct_obs_kernel(const uint32_t *tota
                                                             const int8_t *sem,
                                                             const int32_t *health,
                                                             const float *pos, const float *sur,
+                                                            const int32_t *src_of,
                                                             float *out, uint32_t out_rows)
 {
     __shared__ uint4 s_dep[kObsRows * 2], s_sem[kObsRows * 2];
@@ -1562,17 +1567,28 @@ __global__ __launch_bounds__(256) void construct_obs_kernel(const uint32_t *tota
         else if (t >= 128 && t - 128 < 2 * nr)
             s_sem[t - 128] = reinterpret_cast<const uint4 *>(sem + (size_t)r0 * kSensor)[t - 128];
         if (t < nr) {
-            s_hp[t] = health[r0 + t];
-            s_pos[t] = reinterpret_cast<const float2 *>(pos)[r0 + t];
-            s_sur[t] = reinterpret_cast<const float2 *>(sur)[r0 + t];
+            // (src_of: the deferred Prev move's gather, a newborn's row zero)
+            const int32_t q = src_of ? src_of[r0 + t] : (int32_t)(r0 + t);
+            int32_t hp = 0;
+            float2 ps = make_float2(0.0f, 0.0f), su = ps;
+            if (q >= 0) {
+                hp = health[q];
+                ps = reinterpret_cast<const float2 *>(pos)[q];
+                su = reinterpret_cast<const float2 *>(sur)[q];
+            }
+            s_hp[t] = hp;
+            s_pos[t] = ps;
+            s_sur[t] = su;
         }
         __syncthreads();
         float *o = out + (size_t)r0 * kObsDim;
         if (nr == (uint32_t)kObsRows && (reinterpret_cast<uintptr_t>(out) & 15u) == 0) {
             // 64 x 69 floats = 1104 16-B granules
             for (uint32_t g = t; g < kObsRows * kObsDim / 4; g += 256)
-                reinterpret_cast<float4 *>(o)[g] = make_float4(val(4 * g), val(4 * g + 1), val(4 * g + 2),
-                                                               val(4 * g + 3));
+                st_stream(reinterpret_cast<uint4 *>(o) + g,
+                          make_uint4(__float_as_uint(val(4 * g)), __float_as_uint(val(4 * g + 1)),
+                                     __float_as_uint(val(4 * g + 2)), __float_as_uint(val(4 * g + 3))),
+                          MB_OBS_NT != 0);
         } else {
             for (uint32_t i = t; i < nr * kObsDim; i += 256) o[i] = val(i);
         }
@@ -1647,8 +1663,10 @@ __global__ __launch_bounds__(256) void unpack_rollout_kernel(const uint8_t *recs
         float *o = obs + (size_t)r0 * kObsDim;
         if (nr == (uint32_t)kObsRows && (reinterpret_cast<uintptr_t>(obs) & 15u) == 0) {
             for (uint32_t g = t; g < kObsRows * kObsDim / 4; g += 256)
-                reinterpret_cast<float4 *>(o)[g] = make_float4(val(4 * g), val(4 * g + 1), val(4 * g + 2),
-                                                               val(4 * g + 3));
+                st_stream(reinterpret_cast<uint4 *>(o) + g,
+                          make_uint4(__float_as_uint(val(4 * g)), __float_as_uint(val(4 * g + 1)),
+                                     __float_as_uint(val(4 * g + 2)), __float_as_uint(val(4 * g + 3))),
+                          MB_OBS_NT != 0);
         } else {
             for (uint32_t i = t; i < nr * kObsDim; i += 256) o[i] = val(i);
         }
@@ -1780,12 +1798,22 @@ __global__ __launch_bounds__(256) void synthetic_actions_kernel(SimState S, ObsT
         ap[0] = make_int2(k == 0, k == 1);
         ap[1] = make_int2(k == 2, k == 3);
         ap[2] = make_int2(k == 4, k == 5);
-        if (write_hidden) {   // both words of each draw: hidden[2k], hidden[2k + 1]
-            float4 *hp = reinterpret_cast<float4 *>(t.hidden + r * kHidden);
-            for (int q = 0; q < kHidden / 4; ++q) {
-                const uint2 a = threefry2x32(seed ^ 0x9E3779B9u, step, gw, (uint32_t)i * (kHidden / 2) + 2u * q);
-                const uint2 b = threefry2x32(seed ^ 0x9E3779B9u, step, gw, (uint32_t)i * (kHidden / 2) + 2u * q + 1u);
-                hp[q] = make_float4(u01(a.x) - 0.5f, u01(a.y) - 0.5f, u01(b.x) - 0.5f, u01(b.y) - 0.5f);
+    }
+    // the learner's memory: draw c of slot i (counter 8 i + c) fills
+    // hidden[2c], hidden[2c + 1] of the slot's row; the n x 8 draws spread
+    // over all 64 lanes (eight lanes per slot, one 64-B row), not eight per
+    // slot lane -- the writer is Threefry-bound
+    if (write_hidden) {
+        constexpr uint32_t kDraws = kHidden / 2;
+        const uint32_t nd = (uint32_t)n * kDraws;
+        for (uint32_t u0 = 0; u0 < nd; u0 += 64) {   // wave-uniform trips (the shuffle)
+            const uint32_t u = u0 + lane, i = u / kDraws, c = u % kDraws;
+            const int32_t rs = __shfl(r0, (int)(i & 63u));
+            if (u < nd) {
+                const size_t r = i < 64 ? (size_t)rs : (size_t)S.obsrow[base + i];
+                const uint2 d = threefry2x32(seed ^ 0x9E3779B9u, step, gw, u);
+                reinterpret_cast<float2 *>(t.hidden + r * kHidden)[c] =
+                    make_float2(u01(d.x) - 0.5f, u01(d.y) - 0.5f);
             }
         }
     }
@@ -1949,7 +1977,8 @@ hipError_t launch_synthetic_actions(const SimState &S, const ObsTable &t, uint32
     return hipGetLastError();
 }
 hipError_t launch_construct_obs(const SimState &S, const ObsTable &t, int prev, int prev_lazy,
-                                float *out, uint32_t out_rows, hipStream_t st)
+                                float *out, uint32_t out_rows, hipStream_t st, const ObsTable *six_src,
+                                int six_lazy)
 {
     // Prev{Health, Position, Surrounding} left lazy by the shift are the current ones
     const bool lz = prev && prev_lazy;
@@ -1957,9 +1986,16 @@ hipError_t launch_construct_obs(const SimState &S, const ObsTable &t, int prev, 
     const int8_t *sem = prev ? t.psem : t.sem;
     const uint8_t *depth = fixd ? (prev ? t.pdepth : t.depth) : reinterpret_cast<const uint8_t *>(sem);
     const unsigned blocks = (unsigned)std::min<uint64_t>((out_rows + kObsRows - 1) / kObsRows, 16384);
+    if (prev && six_src) {   // the step's deferred Prev move of the three columns, gathered here
+        const ObsTable &o = *six_src;
+        hipLaunchKernelGGL(construct_obs_kernel, dim3(std::max(blocks, 1u)), dim3(256), 0, st, S.totals, depth,
+                           sem, six_lazy ? o.health : o.phealth, six_lazy ? o.pos : o.ppos,
+                           six_lazy ? o.sur : o.psur, (const int32_t *)S.src_of, out, out_rows);
+        return hipGetLastError();
+    }
     hipLaunchKernelGGL(construct_obs_kernel, dim3(std::max(blocks, 1u)), dim3(256), 0, st, S.totals, depth, sem,
                        prev && !lz ? t.phealth : t.health, prev && !lz ? t.ppos : t.pos,
-                       prev && !lz ? t.psur : t.sur,
+                       prev && !lz ? t.psur : t.sur, (const int32_t *)nullptr,
                        out, out_rows);
     return hipGetLastError();
 }

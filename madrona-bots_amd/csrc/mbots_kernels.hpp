@@ -90,8 +90,12 @@ hipError_t launch_shift(const SimState &S, const ObsTable &t, int mode, hipStrea
 hipError_t launch_synthetic_actions(const SimState &S, const ObsTable &t, uint32_t seed,
                                     uint32_t step, int write_hidden, hipStream_t st);
 hipError_t launch_sensor_index(const SimState &S, int32_t *out, hipStream_t st);
+// six_src: the other half, when the current half's six Prev* columns are
+// still the step's deferred move (prev rows gather their three columns along
+// src_of, as the move would; six_lazy: that move's source is its current ones)
 hipError_t launch_construct_obs(const SimState &S, const ObsTable &t, int prev, int prev_lazy,
-                                float *out, uint32_t out_rows, hipStream_t st);
+                                float *out, uint32_t out_rows, hipStream_t st,
+                                const ObsTable *six_src = nullptr, int six_lazy = 0);
 // rollout records of the config-5 gather (MBOTS_ROLLOUT_BYTES[_DEPTH])
 constexpr uint32_t kRolloutBytes = 64, kRolloutBytesDepth = 96;
 hipError_t launch_pack_rollout(const SimState &S, const ObsTable &t, void *out, uint32_t out_rows,

@@ -920,12 +920,19 @@ int mbots_construct_obs(mbots_handle *h, int32_t prev, float *out, uint64_t out_
     int rc;
     const int owed = pending_mask(h);
     if (!prev && (rc = wait_sensor(h))) return rc;   // current semantic rows come from K3b
-    if (prev && h->six_pending[h->tb] && (rc = materialize_prev(h, st))) return rc;
+    // The previous rows' health / position / surrounding: while the step's
+    // deferred move of the six Prev* columns is still owed, gathered from the
+    // other half along src_of inside this launch (what the move would write,
+    // nothing materialised: the shift that follows in training_loop.py:135
+    // makes the six the current columns, so the move is never run); the prev
+    // sensor is moved (and remembered for the next step's prefetch)
+    const bool gather6 = prev && h->six_pending[h->tb];
     if (prev && (rc = materialize_psem(h, st))) return rc;
-    if (prev) note_use(h, mbots::kMovePrev6 | mbots::kMoveSensor, owed);
+    if (prev) note_use(h, mbots::kMoveSensor, owed);
     return timed(h, MBOTS_TK_OBS, st, [&] {
         return mbots::launch_construct_obs(h->S, h->T[h->tb], prev, h->prev_lazy[h->tb] ? 1 : 0, out,
-                                           (uint32_t)out_rows, st);
+                                           (uint32_t)out_rows, st, gather6 ? &h->T[h->tb ^ 1] : nullptr,
+                                           h->six_lazy[h->tb] ? 1 : 0);
     });
 }
 

@@ -52,3 +52,37 @@ def test_fused_obs_out_buffer():
     assert torch.all(buf[n:] == -7.0)
     with pytest.raises(ValueError):
         sim.construct_obs(False, out=torch.empty((n - 1, rollout.OBS_DIM), device="cuda"))
+
+
+@pytest.mark.gpu
+def test_prev_obs_gathers_the_deferred_move():
+    """construct_obs(True) right after step(), with no Prev* view read in
+    between (the reference loop's pattern, training_loop.py:86): the six Prev*
+    columns are still the step's deferred move, so the kernel gathers health /
+    position / surrounding from the other half along src_of (newborn rows
+    zero).  Compared bit for bit with the CPU mode, which moves eagerly, every
+    step; a breed-heavy action stream makes newborn rows."""
+    import madrona_bots as mb
+    hip = mb.SimManager(0, 256, 69, 32)
+    cpu = mb.SimManager(0, 256, 69, 32, exec_mode="cpu")
+    for m in (hip, cpu):
+        m.write_synthetic_actions(1234, 0, True)
+    for t in range(10):
+        for m in (hip, cpu):
+            m.step()
+        assert hip.num_agents() == cpu.num_agents()
+        for prev in (True, False):
+            a = hip.construct_obs(prev).cpu()
+            b = cpu.construct_obs(prev)
+            assert torch.equal(_bits(a), _bits(b)), (t, prev)
+        for m in (hip, cpu):
+            m.shift_observations()
+            m.write_synthetic_actions(1234, t + 1, True)
+    # and the columns a later accessor materialises agree as well
+    hip.step(); cpu.step()
+    a = hip.construct_obs(True).cpu()
+    assert torch.equal(_bits(a), _bits(cpu.construct_obs(True)))
+    for k in ("position_tensor", "health_tensor", "surrounding_tensor"):
+        x = getattr(hip, k)(True).to_torch().cpu()
+        y = getattr(cpu, k)(True).to_torch()
+        assert torch.equal(x.contiguous().view(torch.int32), y.contiguous().view(torch.int32)), k
