@@ -343,7 +343,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true",
                     help="skip the untimed per-kernel event pass after the timed region")
-    ap.add_argument("--span-every", type=int, default=4,
+    ap.add_argument("--span-every", type=int, default=8,
                     help="bracket every k-th timed step()+shift() with HIP events (roofline "
                          "launch duration); each event pair adds ~10 us of GPU idle")
     ap.add_argument("--gather", action="store_true",
