@@ -641,6 +641,11 @@ int mbots_step(mbots_handle *h, void *stream)
                     [&] { return mbots::launch_world_step(h->S, cur, par, st); })))
         return rc;
     mbots::swap_state(h->S);
+#ifdef MB_PROBE_FORK_K1   // (timing probe only: the sensor reads a stale row_base -- wrong rows)
+    static hipEvent_t ev_k1 = nullptr;
+    if (!ev_k1) HIP_TRY(hipEventCreateWithFlags(&ev_k1, hipEventDisableTiming));
+    HIP_TRY(hipEventRecord(ev_k1, st));
+#endif
     // K2 writes the row counts into the pinned mirror; accessors and the
     // sensor's stream wait on ev_totals, carried by K2's own dispatch
     // (under stream capture -- a caller recording steps into a HIP graph -- the
@@ -664,7 +669,11 @@ int mbots_step(mbots_handle *h, void *stream)
     // writes -- none of which reads the sensor rows or the finder slots.  The
     // next step's K1 and the semantic/depth accessors wait for ev_join.
     const int jcur = h->last_join == 0 ? 1 : 0;
+#ifdef MB_PROBE_FORK_K1
+    HIP_TRY(hipStreamWaitEvent(h->aux, ev_k1, 0));
+#else
     HIP_TRY(hipStreamWaitEvent(h->aux, h->ev_totals, 0));
+#endif
     if ((rc = timed(h, MBOTS_TK_SENSOR, h->aux,
                     [&] { return mbots::launch_sensor(h->S, nxt, h->aux, h->ev_join[jcur], capturing); })))
         return rc;
