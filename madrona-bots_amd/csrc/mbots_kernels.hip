@@ -1197,26 +1197,29 @@ constexpr int kSensorWorlds = MB_SENSOR_WPB;   // worlds (waves) per sensor bloc
 #ifndef MB_SENSOR_SPLIT
 #define MB_SENSOR_SPLIT 4          // waves per world of the split sensor
 #endif
-#ifndef MB_SENSOR_BLOCKS
-#define MB_SENSOR_BLOCKS 8   // min blocks per CU in the launch bounds: <= 64 VGPRs, 8 waves/SIMD
+#ifndef MB_SENSOR_SPLIT_WAVES
+#define MB_SENSOR_SPLIT_WAVES MB_SENSOR_WPB   // waves per block of the split sensor
 #endif
+// the launch bounds' minimum waves per SIMD: 8 (<= 64 VGPRs) for the 128-slot
+// class, 4 for the 256-slot one
+__host__ __device__ constexpr int sensor_min_waves(int cap) { return cap <= 128 ? 8 : 4; }
 // kDepth: fix_depth_alias (a depth byte per pixel besides the semantic one).
 // kSplit: kSplit waves share one world, each taking every kSplit-th key chunk
 // (each stages its own LDS image of the world).  Used at small world counts
 // (<= 4096), where one wave per world leaves SIMDs idle and the step waits on
 // the latency of one world's serial chunk loop (4 waves per world: step -8 % at
 // 4096 worlds; 2 waves: -5 %; no gain at 8192).
-template <bool kDepth, int kSplit, int kCap>
-__global__ __launch_bounds__(64 * kSensorWorlds, kCap <= 128 ? MB_SENSOR_BLOCKS : 4) void sensor_kernel(SimState S,
-                                                                                                  ObsTable nxt)
+template <bool kDepth, int kSplit, int kCap, int kWaves>
+__global__ __launch_bounds__(64 * kWaves, sensor_min_waves(kCap)) void sensor_kernel(SimState S,
+                                                                                            ObsTable nxt)
 {
     constexpr int kG = kCap / 64;   // 64-slot groups
-    __shared__ SensorLDS<kCap> lds[kSensorWorlds];
+    __shared__ SensorLDS<kCap> lds[kWaves];
     __shared__ RayTab R;
     const uint32_t wv = threadIdx.x >> 6;
     const uint32_t lane = threadIdx.x & 63u;
-    static_assert(kSensorWorlds % kSplit == 0, "split must divide the block's waves");
-    const uint32_t w = uniform(blockIdx.x * (kSensorWorlds / kSplit) + wv / kSplit);
+    static_assert(kWaves % kSplit == 0, "split must divide the block's waves");
+    const uint32_t w = uniform(blockIdx.x * (kWaves / kSplit) + wv / kSplit);
     constexpr int kChunkStep = kKeyAgents * kSplit;
     const int kChunk0 = (int)(wv % kSplit) * kKeyAgents;
     if (w >= S.W) return;
@@ -1945,16 +1948,17 @@ static void launch_sensor_cap(const SimState &S, const ObsTable &nxt, hipStream_
                               bool plain_events)
 {
     const bool fixd = (S.flags & kFlagFixDepth) != 0;
-    const dim3 blk(64 * kSensorWorlds);
     if (S.W <= (uint32_t)MB_SENSOR_SPLIT_MAX) {   // small: MB_SENSOR_SPLIT waves per world
-        constexpr int kWpb = kSensorWorlds / MB_SENSOR_SPLIT;
-        const dim3 grid((S.W + kWpb - 1) / kWpb);
-        if (fixd) MB_LAUNCH_EV((sensor_kernel<true, MB_SENSOR_SPLIT, kCap>), grid, blk, st, done, plain_events, S, nxt);
-        else MB_LAUNCH_EV((sensor_kernel<false, MB_SENSOR_SPLIT, kCap>), grid, blk, st, done, plain_events, S, nxt);
+        constexpr int kWv = MB_SENSOR_SPLIT_WAVES, kWpb = kWv / MB_SENSOR_SPLIT;
+        const dim3 grid((S.W + kWpb - 1) / kWpb), blk(64 * kWv);
+        if (fixd)
+            MB_LAUNCH_EV((sensor_kernel<true, MB_SENSOR_SPLIT, kCap, kWv>), grid, blk, st, done, plain_events, S, nxt);
+        else
+            MB_LAUNCH_EV((sensor_kernel<false, MB_SENSOR_SPLIT, kCap, kWv>), grid, blk, st, done, plain_events, S, nxt);
     } else {
-        const dim3 grid((S.W + kSensorWorlds - 1) / kSensorWorlds);
-        if (fixd) MB_LAUNCH_EV((sensor_kernel<true, 1, kCap>), grid, blk, st, done, plain_events, S, nxt);
-        else MB_LAUNCH_EV((sensor_kernel<false, 1, kCap>), grid, blk, st, done, plain_events, S, nxt);
+        const dim3 grid((S.W + kSensorWorlds - 1) / kSensorWorlds), blk(64 * kSensorWorlds);
+        if (fixd) MB_LAUNCH_EV((sensor_kernel<true, 1, kCap, kSensorWorlds>), grid, blk, st, done, plain_events, S, nxt);
+        else MB_LAUNCH_EV((sensor_kernel<false, 1, kCap, kSensorWorlds>), grid, blk, st, done, plain_events, S, nxt);
     }
 }
 hipError_t launch_sensor(const SimState &S, const ObsTable &nxt, hipStream_t st, hipEvent_t done,
