@@ -952,7 +952,8 @@ struct SensorLDS {
     float2 obj[kMaxFood + kCap + (kCap <= 128 ? 64 : 0)];
     float2 frot[kMaxFood];                    // food squares' (cos, sin)
     float2 hd[kCap];                          // agent headings
-    int8_t sp[kCap];
+    int8_t sem_of[kOrderAgent + kCap];        // semantic byte by object order: food 6,
+                                              // agent 64 + slot its species
     alignas(16) uint32_t key[kKeyAgents * kKeyStride];
     uint32_t qcode[kQueueCap + 1];            // P1 survivors: agent | object << 11 (+ a
                                               // sink slot for the branch-free write); a
@@ -1225,16 +1226,12 @@ __global__ __launch_bounds__(64 * kWaves, sensor_min_waves(kCap)) void sensor_ke
     if (w >= S.W) return;
     SensorLDS<kCap> &L = lds[wv];
     constexpr bool depth = kDepth;
-    if (lane <= kSensor) {   // ray `lane` (the finder at u = 0: near_pt(0) = {1.1, 0, 1.1})
-        const float u = lane < kSensor ? u_of((int)lane) : 0.0f;
-        const NearPt np = near_pt(u);
-        R.u[lane] = u;
-        R.c[lane] = np.c;
-        R.s[lane] = np.s;
-        R.e[lane] = np.e;
-    }
     SensorPrefetch pf;
     sensor_prefetch(S, w, lane, pf);
+    // ray `lane`'s u and near point (the finder at 32: u = 0, {1.1, 0, 1.1}),
+    // host-computed (upload_ray_table), loaded with the prefetch batch and
+    // stored to the block's table after the staging below
+    const float4 ray = lane <= (uint32_t)kSensor ? S.raytab[lane] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     {
     const size_t base = (size_t)w * S.cap;
     const SensorPrefetch cur = pf;
@@ -1251,12 +1248,13 @@ __global__ __launch_bounds__(64 * kWaves, sensor_min_waves(kCap)) void sensor_ke
     }
     const int nf = stage_food(cur.food, rot, lane, L.obj, L.frot);
     // ---- agents -> objects [nf, nf + n) ----
+    L.sem_of[lane] = 6;   // orders < 64: wall 0 (unused), food 1 + k
     if ((int)lane < n) {
         float hx, hy;
         heading(cur.rw, cur.rz, hx, hy);
         L.obj[nf + lane] = make_float2(cur.x, cur.y);
         L.hd[lane] = make_float2(hx, hy);
-        L.sp[lane] = (int8_t)cur.sp;
+        L.sem_of[kOrderAgent + lane] = (int8_t)cur.sp;
     }
     // export rows (K3a's rule, computed here so the sensor need not wait for
     // K3a): row_base[w][species] + rank among the world's slots of that
@@ -1278,7 +1276,7 @@ __global__ __launch_bounds__(64 * kWaves, sensor_min_waves(kCap)) void sensor_ke
             L.obj[nf + i] = make_float2(S.x[base + i], S.y[base + i]);
             L.hd[i] = make_float2(hx, hy);
             sp = S.species[base + i];
-            L.sp[i] = (int8_t)sp;
+            L.sem_of[kOrderAgent + i] = (int8_t)sp;
         }
         const uint64_t m1 = ballot64(sp == 1), m2 = ballot64(sp == 2);
         const uint64_t m3 = ballot64(sp == 3), m4 = ballot64(sp == 4);
@@ -1291,6 +1289,12 @@ __global__ __launch_bounds__(64 * kWaves, sensor_min_waves(kCap)) void sensor_ke
     // the pair loop needs no bounds check or clamped read (j < nobj + 63)
     constexpr bool kPad = kCap <= 128;
     if (kPad) L.obj[nobj + (int)lane] = make_float2(__builtin_nanf(""), __builtin_nanf(""));
+    if (lane <= (uint32_t)kSensor) {   // every wave stores the same bits: no barrier
+        R.u[lane] = ray.x;
+        R.c[lane] = ray.y;
+        R.s[lane] = ray.z;
+        R.e[lane] = ray.w;
+    }
     wave_sync();
 
     uint32_t mbc = 0;
@@ -1415,9 +1419,8 @@ __global__ __launch_bounds__(64 * kWaves, sensor_min_waves(kCap)) void sensor_ke
                 const float oz = __uint_as_float(kv & ~kOrderMask);
                 const uint32_t order = kv & kOrderMask;
                 const bool obj = (kv != kNoKey) & beats_wall_in(lox, hix, loy, hiy, dx, dy, oz);
-                // (any index in range: the species is used only for an agent's order)
-                const int spv = (int)L.sp[(order - kOrderAgent) & (kCap - 1)];
-                const int sem = obj ? (order < kOrderAgent ? 6 : spv) : 5;
+                // (read for any key: a miss's order bits 0x1FF clamp into the table)
+                const int sem = obj ? (int)L.sem_of[min(order, (uint32_t)(kOrderAgent + kCap - 1))] : 5;
                 semv |= (uint32_t)(uint8_t)(int8_t)sem << (8 * t);
                 if (depth) {
                     const float z = obj ? oz : wall_z(p.x, p.y, dx, dy);
@@ -1485,8 +1488,7 @@ __global__ __launch_bounds__(64 * kWaves, sensor_min_waves(kCap)) void sensor_ke
                     const float hxs = fw ? h.x : -h.x, hys = fw ? h.y : -h.y;
                     const float dx = hxs + u * hys, dy = hys + u * (-hxs);
                     const bool obj = (kv != kNoKey) & (none | (inner && beats_wall(p.x, p.y, dx, dy, oz)));
-                    const int spv = (int)L.sp[(order - kOrderAgent) & (kCap - 1)];
-                    const int sem = obj ? (order < kOrderAgent ? 6 : spv) : (none ? -1 : 5);
+                    const int sem = obj ? (int)L.sem_of[min(order, (uint32_t)(kOrderAgent + kCap - 1))] : (none ? -1 : 5);
                     nxt.sem[(size_t)r * kSensor + k] = (int8_t)sem;
                     if (depth) {
                         const float z = obj ? oz : none ? __builtin_inff() : inner ? wall_z(p.x, p.y, dx, dy) : c;
@@ -1840,6 +1842,19 @@ __global__ __launch_bounds__(256) void sensor_index_kernel(SimState S, int32_t *
 static inline unsigned world_blocks(uint32_t W) { return (W + kWorldsPerBlock - 1) / kWorldsPerBlock; }
 
 uint32_t scan_tiles(uint32_t W) { return (W + kTileWorlds - 1) / kTileWorlds; }
+
+hipError_t upload_ray_table(const SimState &S, hipStream_t st)
+{
+    // the same float expressions on the host (IEEE sqrt / division, no
+    // contraction): the table's bits are the ones the kernel computed itself
+    static float4 tab[36];
+    for (int k = 0; k < 36; ++k) {
+        const float u = k < kSensor ? u_of(k) : 0.0f;
+        const NearPt np = near_pt(u);
+        tab[k] = make_float4(u, np.c, np.s, np.e);
+    }
+    return hipMemcpyAsync(S.raytab, tab, sizeof(tab), hipMemcpyHostToDevice, st);
+}
 
 hipError_t launch_init(const SimState &S, hipStream_t st)
 {

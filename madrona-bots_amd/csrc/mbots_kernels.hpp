@@ -35,6 +35,7 @@ struct SimState {
     uint32_t *totals_host;          // mapped pinned mirror of totals (written by K2)
     int32_t *tiles;                 // [2][5][ntiles][kTileBuckets] per-tile species/agent counts (K1 -> K2)
     unsigned long long *agent_steps;
+    float4 *raytab;                 // [36] per ray (32 pixels, the finder): u, NearPt c, s, e
     // K1's output half of the double-buffered columns the sensor reads (the
     // sensor of step t runs beside step t+1's K1; swap_state after each K1)
     float *x_out, *y_out, *rw_out, *rz_out;
@@ -68,6 +69,8 @@ uint32_t scan_tiles(uint32_t W);
 // counters (block index mod 8): fewer same-address atomics at K1's end
 constexpr int kTileBuckets = 8;
 hipError_t launch_init(const SimState &S, hipStream_t st);
+// the sensor's ray table (host-computed with the kernels' own u_of / near_pt)
+hipError_t upload_ray_table(const SimState &S, hipStream_t st);
 hipError_t launch_tile_sum(const SimState &S, int parity, hipStream_t st);
 hipError_t launch_world_step(const SimState &S, const ObsTable &cur, int parity, hipStream_t st);
 // plain_events: record `done` with hipEventRecord (stream capture) instead of on the dispatch

@@ -199,6 +199,7 @@ size_t layout(mbots_handle *h, Arena &a)
     S.ntiles = scan_tiles((uint32_t)W);
     S.tiles = a.take<int32_t>((size_t)2 * S.ntiles * kTileBuckets * 5);
     S.agent_steps = a.take<unsigned long long>(1);
+    S.raytab = a.take<float4>(36);
     S.x_out = a.take<float>(rows);
     S.y_out = a.take<float>(rows);
     S.rw_out = a.take<float>(rows);
@@ -550,6 +551,7 @@ int mbots_create(const mbots_config *cfg_in, mbots_handle **out)
     hipStream_t st = nullptr;
     check(hipMemsetAsync(h->arena.base, 0, bytes, st), "hipMemsetAsync");
     // Sim::Sim / initWorld (sim.cpp:1232-1256) + initial export of the rows
+    check(mbots::upload_ray_table(S, st), "upload_ray_table");
     check(mbots::launch_init(S, st), "init_kernel");
     check(mbots::launch_tile_sum(S, 0, st), "tile_sum_kernel");
     check(mbots::launch_scan(S, 0, st), "scan_kernel");
