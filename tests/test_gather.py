@@ -126,3 +126,49 @@ def test_gather_records_two_cpu_shards_equal_one(fix_depth):
         assert p.exitcode == 0
     ok = q.get(timeout=5)
     assert all(ok.values()), ok
+
+
+def _rccl_worker(port, q):
+    sys.path[:0] = [HARNESS, os.path.join(ROOT, "madrona-bots_amd")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        import gather
+        import madrona_bots as mb
+        sim = mb.SimManager(0, 512, SEED, 32)
+        for t in range(STEPS):
+            sim.write_synthetic_actions(1234, t, True)
+            sim.step()
+            if t < STEPS - 1:
+                sim.shift_observations()
+        out = gather.gather_records(sim, dst=0)
+        ref = {"obs": sim.construct_obs(False), "reward": sim.reward_tensor(False).to_torch(),
+               "stats": sim.stats_tensor(False).to_torch()}
+        torch.cuda.synchronize()
+        q.put({k: bool(torch.equal(out[k].view(torch.int32).cpu(), ref[k].contiguous().view(torch.int32).cpu()))
+               for k in ref})
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_gather_records_over_rccl_one_rank():
+    """The config-5 gather's collectives (all_gather of the species counts,
+    gather of the packed records) executed by RCCL (the nccl backend) on the
+    device, one rank: the rows rebuilt from the gathered records equal the
+    manager's own construct_obs / reward / stats bitwise.  (Several ranks need
+    several GPUs: the driver's multi-GPU bench runs that; tests/test_gather's
+    gloo cases cover the reassembly across shards.)"""
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_rccl_worker, args=(port, q))
+    p.start()
+    p.join(timeout=240)
+    assert p.exitcode == 0
+    ok = q.get(timeout=5)
+    assert all(ok.values()), ok
