@@ -1047,7 +1047,7 @@ __device__ __forceinline__ void run_survivors(LDS &L, const RayTab &R, int nf, i
     MB_CNT(4, cnt);
 #ifdef MB_COUNT
     int mb_t = 0;
-    bool mb_food = false;
+    bool mb_food = false, mb_disc = false;
 #endif
     const int lane = (int)__lane_id();
     bool wide = false;
@@ -1131,6 +1131,7 @@ __device__ __forceinline__ void run_survivors(LDS &L, const RayTab &R, int nf, i
 #ifdef MB_COUNT
             mb_t = max(kl - k0 - 1, 0);
             mb_food = food;
+            mb_disc = !food;
 #endif
         }
     }
@@ -1143,6 +1144,13 @@ __device__ __forceinline__ void run_survivors(LDS &L, const RayTab &R, int nf, i
     for (int o = 32; o > 0; o >>= 1) mb_t = max(mb_t, __shfl_xor(mb_t, o));
     MB_CNT(7, mb_t);
     MB_CNT(9, __popcll(ballot64(mb_food)));
+    {
+        // batches running the far-square path / the far-disc path / both
+        const uint64_t fm = ballot64(mb_food), dm = ballot64(mb_disc);
+        MB_CNT(10, fm != 0ull);
+        MB_CNT(11, dm != 0ull);
+        MB_CNT(12, (fm != 0ull) & (dm != 0ull));
+    }
 #endif
 #ifndef MB_SKIP_WIDE   // (instruction-count probes only: MB_SKIP_* builds give wrong rows)
     if (nw > 0) {
