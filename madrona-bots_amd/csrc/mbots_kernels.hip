@@ -1324,22 +1324,33 @@ __global__ __launch_bounds__(64 * kWaves, sensor_min_waves(kCap)) void sensor_ke
             const float2 ap = a < nc ? L.obj[nf + ia] : make_float2(__builtin_nanf(""), __builtin_nanf(""));
             const float2 ah = L.hd[ia];
             const int self = nf + ia;
-            for (int jb = 0; jb < nobj; jb += G) {
+            // the camera's own projections, so (f, l) of an object p are two
+            // FMAs each: f = p.h - c, l = p.r - d (r = (hy, -hx)).  An
+            // approximation of pair_fl's (f, l) within ~1e-5 (|p|, |a| <= 160):
+            // the wedge's + 0.05 and the angular cull's 1e-4 margin in u
+            // (>= 1e-4 |f| in l) dwarf it; survivors recompute exactly.  (A NaN
+            // camera gives NaN c, d: every test fails.)
+            const float pc = __builtin_fmaf(ap.x, ah.x, ap.y * ah.y);
+            const float pd = __builtin_fmaf(ap.x, ah.y, -(ap.y * ah.x));
+            // body of one P1 iteration; kKind 0: every lane's object is food
+            // (j + G <= nf), 1: every one an agent (j >= nf), 2: mixed -- the
+            // radius and the self test then compile out of the uniform kinds
+            auto p1_iter = [&](const int jb, auto kind_tag) {
+                constexpr int kKind = decltype(kind_tag)::value;
                 MB_CNT(2, 1);
                 const int j = jb + o;
                 // (j >= nobj reads a NaN sentinel: keep comes out false)
                 const float2 p = L.obj[kPad ? j : min(j, nobj - 1)];
-                const float vx = p.x - ap.x, vy = p.y - ap.y;
-                // pair_fl's (f, l) up to an FMA rounding: the cull's margin
-                // (the wedge's + 0.05) dwarfs it; survivors recompute exactly
-                const float f = __builtin_fmaf(vx, ah.x, vy * ah.y), l = __builtin_fmaf(vx, ah.y, -(vy * ah.x));
-                const bool food = j < nf;
+                const float f = __builtin_fmaf(p.x, ah.x, __builtin_fmaf(p.y, ah.y, -pc));
+                const float l = __builtin_fmaf(p.x, ah.y, __builtin_fmaf(-p.y, ah.x, -pd));
+                const bool food = kKind == 0 ? true : kKind == 1 ? false : j < nf;
                 const float af = fabsf(f);
                 // the object's radius with the cull's 1.001 margin (the wedge's
                 // half-width sqrt(2) rk + 0.05 >= sqrt(2) R + 0.05)
                 const float rk = food ? 1.42f * 1.001f : kAgentR * 1.001f;
-                bool keep = (kPad | (j < nobj)) & (j != self) &
-                            (fabsf(l) <= af + __builtin_fmaf(1.41421356f, rk, 0.05f));
+                const float wk = food ? 1.41421356f * (1.42f * 1.001f) + 0.05f
+                                      : 1.41421356f * (kAgentR * 1.001f) + 0.05f;
+                bool keep = (kPad | (j < nobj)) & (kKind == 0 || j != self) & (fabsf(l) <= af + wk);
                 {
                     // a far pair (|f| >= kFarCull) also needs a pixel centre, or
                     // forward the finder ray u = 0, within w of its centre's
@@ -1378,7 +1389,13 @@ __global__ __launch_bounds__(64 * kWaves, sensor_min_waves(kCap)) void sensor_ke
 #endif
                     nq -= 64;
                 }
-            }
+            };
+            // food iterations, the one straddling nf, agent iterations (the
+            // kind is wave-uniform in all but one iteration per chunk)
+            int jb = 0;
+            for (; jb + G <= nf; jb += G) p1_iter(jb, std::integral_constant<int, 0>{});
+            if (jb < nf) { p1_iter(jb, std::integral_constant<int, 2>{}); jb += G; }
+            for (; jb < nobj; jb += G) p1_iter(jb, std::integral_constant<int, 1>{});
         }
         if (nq > 0) {
             wave_sync();
