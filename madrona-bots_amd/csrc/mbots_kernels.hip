@@ -943,6 +943,9 @@ constexpr float kUEps = 2e-3f;                // root-interval margin in u
 constexpr float kFoodFar = 2.55f;
 constexpr float kCircleFar = 1.5f;
 constexpr float kFarCull = 5.0f;               // P1 angular cull from this |f| on
+#ifndef MB_SPLIT_FLUSH
+#define MB_SPLIT_FLUSH 16   // food survivors flushed alone from this many on (24: +0.2 %, 40: +0.3 %, never: +1 %)
+#endif
 
 template <int kCap>
 struct SensorLDS {
@@ -980,15 +983,17 @@ __host__ __device__ constexpr float u_of(int k)
     return k < 24 ? (float)(2 * k - 23) * (1.0f / 24.0f) : (float)(2 * (k - 24) - 7) * 0.125f;
 }
 
-// (f, l) of object j in agent i's frame; order of the object
+// (f, l) of object j in agent i's frame; order of the object (food at
+// [0, nf), agents from na = nf rounded up to 8; the gap holds NaN, which no
+// queued pair references, so j < na tells food from agents)
 template <class LDS>
-__device__ __forceinline__ void pair_fl(const LDS &L, int nf, int i, int j, float &f,
+__device__ __forceinline__ void pair_fl(const LDS &L, int na, int i, int j, float &f,
                                         float &l, uint32_t &order)
 {
-    const float2 a = L.obj[nf + i];
+    const float2 a = L.obj[na + i];
     const float2 h = L.hd[i];
     const float2 p = L.obj[j];
-    order = j < nf ? kOrderFood + (uint32_t)j : kOrderAgent + (uint32_t)(j - nf);
+    order = j < na ? kOrderFood + (uint32_t)j : kOrderAgent + (uint32_t)(j - na);
     const float vx = p.x - a.x, vy = p.y - a.y;
     f = vx * h.x + vy * h.y;   // along the heading
     l = vx * h.y - vy * h.x;   // along r = (hy, -hx)
@@ -1005,7 +1010,7 @@ __device__ __forceinline__ void pair_fl(const LDS &L, int nf, int i, int j, floa
 #endif
 
 template <class LDS>
-__device__ __forceinline__ void run_wide(LDS &L, const RayTab &R, int nf, int a0, int q0, int cnt, uint32_t &mbc)
+__device__ __forceinline__ void run_wide(LDS &L, const RayTab &R, int na, int a0, int q0, int cnt, uint32_t &mbc)
 {
     MB_CNT(6, (cnt + 1) / 2);
     const int lane = (int)__lane_id();
@@ -1020,10 +1025,10 @@ __device__ __forceinline__ void run_wide(LDS &L, const RayTab &R, int nf, int a0
             const int ic = (int)(code & 0x1Fu), j = (int)(code >> 11);
             float f, l;
             uint32_t order;
-            pair_fl(L, nf, a0 + ic, j, f, l, order);
+            pair_fl(L, na, a0 + ic, j, f, l, order);
             uint32_t *kr = L.key + ic * kKeyStride;
             uint32_t kv, kf;
-            if (j < nf) {   // food square: every ray exactly
+            if (j < na) {   // food square: every ray exactly
                 const FoodBox b = box_setup(f, l, L.frot[j], L.hd[a0 + ic]);
                 kv = box_hit(b, uk, k < 24, np.c) ? zkey(box_z(b, k < 24), order) : kNoKey;
                 kf = box_hit(b, 0.0f, true, fnp.c) ? zkey(box_z(b, true), order) : kNoKey;
@@ -1041,7 +1046,7 @@ __device__ __forceinline__ void run_wide(LDS &L, const RayTab &R, int nf, int a0
 // candidate pixels; the edge pixels and the finder get the exact test inline,
 // near pairs go to the wide list
 template <class LDS>
-__device__ __forceinline__ void run_survivors(LDS &L, const RayTab &R, int nf, int a0, int q0, int cnt, uint32_t &mbc)
+__device__ __forceinline__ void run_survivors(LDS &L, const RayTab &R, int na, int a0, int q0, int cnt, uint32_t &mbc)
 {
     MB_CNT(3, 1);
     MB_CNT(4, cnt);
@@ -1057,8 +1062,8 @@ __device__ __forceinline__ void run_survivors(LDS &L, const RayTab &R, int nf, i
         code = L.qcode[q0 + lane];
         const int ic = (int)(code & 0x1Fu), j = (int)(code >> 11);
         uint32_t order;
-        pair_fl(L, nf, a0 + ic, j, f, l, order);
-        const bool food = j < nf;
+        pair_fl(L, na, a0 + ic, j, f, l, order);
+        const bool food = j < na;
         const float r2 = f * f + l * l;
         if (fabsf(f) <= (food ? kFoodFar : kCircleFar)) {
             wide = true;
@@ -1155,7 +1160,7 @@ __device__ __forceinline__ void run_survivors(LDS &L, const RayTab &R, int nf, i
 #ifndef MB_SKIP_WIDE   // (instruction-count probes only: MB_SKIP_* builds give wrong rows)
     if (nw > 0) {
         wave_sync();
-        run_wide(L, R, nf, a0, q0, nw, mbc);
+        run_wide(L, R, na, a0, q0, nw, mbc);
         wave_sync();
     }
 #endif
@@ -1255,12 +1260,17 @@ __global__ __launch_bounds__(64 * kWaves, sensor_min_waves(kCap)) void sensor_ke
             rot[k] = (live >> k) & 1u ? S.food_rot[(size_t)w * kNumPkg + k * kNumChunks + lane] : 0u;
     }
     const int nf = stage_food(cur.food, rot, lane, L.obj, L.frot);
-    // ---- agents -> objects [nf, nf + n) ----
+    // ---- agents -> objects [na, na + n), na = nf rounded up to 8: P1's
+    // 8-object iterations are then all food or all agents (full chunks), so a
+    // chunk's food survivors can be flushed as their own batch (below); the
+    // gap holds NaN (every P1 test fails) ----
+    const int na = (nf + 7) & ~7;
+    if ((int)lane >= nf && (int)lane < na) L.obj[lane] = make_float2(__builtin_nanf(""), __builtin_nanf(""));
     L.sem_of[lane] = 6;   // orders < 64: wall 0 (unused), food 1 + k
     if ((int)lane < n) {
         float hx, hy;
         heading(cur.rw, cur.rz, hx, hy);
-        L.obj[nf + lane] = make_float2(cur.x, cur.y);
+        L.obj[na + lane] = make_float2(cur.x, cur.y);
         L.hd[lane] = make_float2(hx, hy);
         L.sem_of[kOrderAgent + lane] = (int8_t)cur.sp;
     }
@@ -1281,7 +1291,7 @@ __global__ __launch_bounds__(64 * kWaves, sensor_min_waves(kCap)) void sensor_ke
         } else if (i < n) {   // slots past 64: loaded here
             float hx, hy;
             heading(S.rw[base + i], S.rz[base + i], hx, hy);
-            L.obj[nf + i] = make_float2(S.x[base + i], S.y[base + i]);
+            L.obj[na + i] = make_float2(S.x[base + i], S.y[base + i]);
             L.hd[i] = make_float2(hx, hy);
             sp = S.species[base + i];
             L.sem_of[kOrderAgent + i] = (int8_t)sp;
@@ -1292,7 +1302,7 @@ __global__ __launch_bounds__(64 * kWaves, sensor_min_waves(kCap)) void sensor_ke
                 : sp == 3 ? rb.z + c3 + (int)rank_below(m3) : rb.w + c4 + (int)rank_below(m4);
         c1 += __popcll(m1); c2 += __popcll(m2); c3 += __popcll(m3); c4 += __popcll(m4);
     }
-    const int nobj = nf + n;
+    const int nobj = na + n;
     // sentinels past the last object: a NaN position fails every P1 test, so
     // the pair loop needs no bounds check or clamped read (j < nobj + 63)
     constexpr bool kPad = kCap <= 128;
@@ -1321,9 +1331,9 @@ __global__ __launch_bounds__(64 * kWaves, sensor_min_waves(kCap)) void sensor_ke
             const int a = (int)lane >> lgG, o = (int)lane & (G - 1);
             const int ia = a0 + min(a, nc - 1);
             // a lane past the chunk's agents gets a NaN camera: every test fails
-            const float2 ap = a < nc ? L.obj[nf + ia] : make_float2(__builtin_nanf(""), __builtin_nanf(""));
+            const float2 ap = a < nc ? L.obj[na + ia] : make_float2(__builtin_nanf(""), __builtin_nanf(""));
             const float2 ah = L.hd[ia];
-            const int self = nf + ia;
+            const int self = na + ia;
             // the camera's own projections, so (f, l) of an object p are two
             // FMAs each: f = p.h - c, l = p.r - d (r = (hy, -hx)).  An
             // approximation of pair_fl's (f, l) within ~1e-5 (|p|, |a| <= 160):
@@ -1333,7 +1343,7 @@ __global__ __launch_bounds__(64 * kWaves, sensor_min_waves(kCap)) void sensor_ke
             const float pc = __builtin_fmaf(ap.x, ah.x, ap.y * ah.y);
             const float pd = __builtin_fmaf(ap.x, ah.y, -(ap.y * ah.x));
             // body of one P1 iteration; kKind 0: every lane's object is food
-            // (j + G <= nf), 1: every one an agent (j >= nf), 2: mixed -- the
+            // (j + G <= na), 1: every one an agent (j >= na), 2: mixed -- the
             // radius and the self test then compile out of the uniform kinds
             auto p1_iter = [&](const int jb, auto kind_tag) {
                 constexpr int kKind = decltype(kind_tag)::value;
@@ -1343,7 +1353,7 @@ __global__ __launch_bounds__(64 * kWaves, sensor_min_waves(kCap)) void sensor_ke
                 const float2 p = L.obj[kPad ? j : min(j, nobj - 1)];
                 const float f = __builtin_fmaf(p.x, ah.x, __builtin_fmaf(p.y, ah.y, -pc));
                 const float l = __builtin_fmaf(p.x, ah.y, __builtin_fmaf(-p.y, ah.x, -pd));
-                const bool food = kKind == 0 ? true : kKind == 1 ? false : j < nf;
+                const bool food = kKind == 0 ? true : kKind == 1 ? false : j < na;
                 const float af = fabsf(f);
                 // the object's radius with the cull's 1.001 margin (the wedge's
                 // half-width sqrt(2) rk + 0.05 >= sqrt(2) R + 0.05)
@@ -1385,22 +1395,32 @@ __global__ __launch_bounds__(64 * kWaves, sensor_min_waves(kCap)) void sensor_ke
                 if (nq >= 64) {
                     wave_sync();
 #ifndef MB_SKIP_P2
-                    run_survivors(L, R, nf, a0, nq - 64, 64, mbc);
+                    run_survivors(L, R, na, a0, nq - 64, 64, mbc);
 #endif
                     nq -= 64;
                 }
             };
-            // food iterations, the one straddling nf, agent iterations (the
-            // kind is wave-uniform in all but one iteration per chunk)
+            // food iterations, the one straddling na (none for full chunks: G
+            // = 8 divides na), agent iterations
             int jb = 0;
-            for (; jb + G <= nf; jb += G) p1_iter(jb, std::integral_constant<int, 0>{});
-            if (jb < nf) { p1_iter(jb, std::integral_constant<int, 2>{}); jb += G; }
+            for (; jb + G <= na; jb += G) p1_iter(jb, std::integral_constant<int, 0>{});
+            if (jb < na) { p1_iter(jb, std::integral_constant<int, 2>{}); jb += G; }
+            // the food survivors as a batch of their own when the agents'
+            // would fill another anyway: a batch mixing far squares and far
+            // discs runs both paths (and so do its near-pair rounds)
+            if (nq >= MB_SPLIT_FLUSH) {
+                wave_sync();
+#ifndef MB_SKIP_P2
+                run_survivors(L, R, na, a0, 0, nq, mbc);
+#endif
+                nq = 0;
+            }
             for (; jb < nobj; jb += G) p1_iter(jb, std::integral_constant<int, 1>{});
         }
         if (nq > 0) {
             wave_sync();
 #ifndef MB_SKIP_P2
-            run_survivors(L, R, nf, a0, 0, nq, mbc);
+            run_survivors(L, R, na, a0, 0, nq, mbc);
 #endif
         }
         wave_sync();
@@ -1410,7 +1430,7 @@ __global__ __launch_bounds__(64 * kWaves, sensor_min_waves(kCap)) void sensor_ke
             const int ci = (int)(lane >> 3), g = (int)(lane & 7u);
             const int cc = min(ci, nc - 1);
             const int i = a0 + cc;
-            const float2 p = L.obj[nf + i], h = L.hd[i];
+            const float2 p = L.obj[na + i], h = L.hd[i];
             const uint4 kv4 = *reinterpret_cast<const uint4 *>(&L.key[cc * kKeyStride + 4 * g]);
             const float4 u4 = *reinterpret_cast<const float4 *>(&R.u[4 * g]);
             // the chunk's 64-slot group (8 | 64: one group per chunk), a uniform branch
@@ -1461,7 +1481,7 @@ __global__ __launch_bounds__(64 * kWaves, sensor_min_waves(kCap)) void sensor_ke
         bool shallow = false;   // lane a < nc: agent a0 + a is within 1.2 of the inner rectangle's edge
         if ((int)lane < nc) {
             const int i = a0 + (int)lane;
-            const float2 p = L.obj[nf + i], h = L.hd[i];
+            const float2 p = L.obj[na + i], h = L.hd[i];
             const uint32_t kv = L.key[lane * kKeyStride + kSensor];
             const uint32_t order = kv & kOrderMask;
 #ifndef MB_PROBE_ALL_DEEP   // (instruction-count probe: wrong rows near the walls)
@@ -1498,7 +1518,7 @@ __global__ __launch_bounds__(64 * kWaves, sensor_min_waves(kCap)) void sensor_ke
             }
             if (ca >= 0) {
                 const int k = (int)(lane & 31u);
-                const float2 p = L.obj[nf + i], h = L.hd[i];
+                const float2 p = L.obj[na + i], h = L.hd[i];
                 const bool fw = k < 24;
                 const float c = R.c[k], sn = R.s[k];
                 const float ex = c * h.x + sn * h.y, ey = c * h.y + sn * (-h.x);
