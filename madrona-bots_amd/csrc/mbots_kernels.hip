@@ -587,6 +587,7 @@ __global__ __launch_bounds__(1024) void scan_kernel(SimState S, int parity)
 {
     __shared__ int32_t s_pre[5], s_tot[5];
     __shared__ int32_t s_wave[16][5];
+    __shared__ int32_t s_hist[256];
     const int t = threadIdx.x, b = blockIdx.x;
     const int wv = t >> 6, lane = t & 63;
     const uint32_t nent = S.ntiles * kTileBuckets;   // a multiple of 8: 16-B words
@@ -621,12 +622,31 @@ __global__ __launch_bounds__(1024) void scan_kernel(SimState S, int parity)
 #pragma unroll
         for (int k = 0; k < 5; ++k) s_wave[wv][k] = inc[k];
     }
+    // the sensor's dispatch order (S.sorder, when set): the tile's worlds by
+    // descending population, a counting sort on 255 - min(n, 255) (ties in any
+    // order: a world's rows do not depend on when it is rendered)
+    int key = 0, slot = 0;
+    if (S.sorder) {
+        if (t < 256) s_hist[t] = 0;
+        __syncthreads();
+        if (w < S.W) {
+            key = 255 - min(c[4], 255);
+            slot = atomicAdd(&s_hist[key], 1);
+        }
+    }
     __syncthreads();
     if (t < 5) {
         int32_t run = 0;
         for (int i = 0; i < 16; ++i) { const int32_t v = s_wave[i][t]; s_wave[i][t] = run; run += v; }
     }
+    if (S.sorder && wv == 15) {   // exclusive scan of the 256 bins, four per lane
+        const int4 h4 = reinterpret_cast<const int4 *>(s_hist)[lane];
+        const int sum = h4.x + h4.y + h4.z + h4.w;
+        const int ex = wave_incl_scan(sum) - sum;
+        reinterpret_cast<int4 *>(s_hist)[lane] = make_int4(ex, ex + h4.x, ex + h4.x + h4.y, ex + h4.x + h4.y + h4.z);
+    }
     __syncthreads();
+    if (S.sorder && w < S.W) S.sorder[(size_t)b * kTileWorlds + s_hist[key] + slot] = (int32_t)w;
     if (w < S.W) {
         int32_t ex[5];
 #pragma unroll
@@ -1233,7 +1253,16 @@ __global__ __launch_bounds__(64 * kWaves, sensor_min_waves(kCap)) void sensor_ke
     const uint32_t wv = threadIdx.x >> 6;
     const uint32_t lane = threadIdx.x & 63u;
     static_assert(kWaves % kSplit == 0, "split must divide the block's waves");
-    const uint32_t w = uniform(blockIdx.x * (kWaves / kSplit) + wv / kSplit);
+    uint32_t w = blockIdx.x * (kWaves / kSplit) + wv / kSplit;
+    if (kSplit == 1 && S.sorder) {
+        // blocks in dispatch order take every tile's heaviest quad of worlds
+        // first, its lightest last (block b: tile b % ntiles, quad b / ntiles;
+        // used when every tile is full), so the kernel's drain runs the
+        // cheapest worlds and a block's four worlds cost about the same
+        const uint32_t b = blockIdx.x, tile = b % S.ntiles, q = b / S.ntiles;
+        w = (uint32_t)S.sorder[(size_t)tile * kTileWorlds + q * kWaves + wv];
+    }
+    w = uniform(w);
     constexpr int kChunkStep = kKeyAgents * kSplit;
     const int kChunk0 = (int)(wv % kSplit) * kKeyAgents;
     if (w >= S.W) return;
@@ -1887,6 +1916,14 @@ __global__ __launch_bounds__(256) void sensor_index_kernel(SimState S, int32_t *
 static inline unsigned world_blocks(uint32_t W) { return (W + kWorldsPerBlock - 1) / kWorldsPerBlock; }
 
 uint32_t scan_tiles(uint32_t W) { return (W + kTileWorlds - 1) / kTileWorlds; }
+bool sensor_order_used(uint32_t W)
+{
+#ifdef MB_NO_SENSOR_ORDER
+    return false;
+#else
+    return W > (uint32_t)MB_SENSOR_SPLIT_MAX && W % kTileWorlds == 0 && kSensorWorlds * 256 == kTileWorlds;
+#endif
+}
 
 hipError_t upload_ray_table(const SimState &S, hipStream_t st)
 {

@@ -200,6 +200,7 @@ size_t layout(mbots_handle *h, Arena &a)
     S.tiles = a.take<int32_t>((size_t)2 * S.ntiles * kTileBuckets * 5);
     S.agent_steps = a.take<unsigned long long>(1);
     S.raytab = a.take<float4>(36);
+    S.sorder = sensor_order_used((uint32_t)W) ? a.take<int32_t>(W) : nullptr;
     S.x_out = a.take<float>(rows);
     S.y_out = a.take<float>(rows);
     S.rw_out = a.take<float>(rows);
@@ -637,8 +638,10 @@ int mbots_step(mbots_handle *h, void *stream)
         if (cap_id != h->cap_seen) { h->cap_seen = cap_id; h->cap_steps = 0; }
         ++h->cap_steps;
     }
+#ifndef MB_PROBE_NO_JOIN   // (timing probe only: K1 overwrites the state the sensor reads)
     if (h->last_join >= 0 && (!capturing || h->join_capture == cap_id))
         HIP_TRY(hipStreamWaitEvent(st, h->ev_join[h->last_join], 0));
+#endif
     if ((rc = timed(h, MBOTS_TK_WORLD_STEP, st,
                     [&] { return mbots::launch_world_step(h->S, cur, par, st); })))
         return rc;
