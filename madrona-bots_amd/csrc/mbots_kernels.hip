@@ -1253,14 +1253,15 @@ __global__ __launch_bounds__(64 * kWaves, sensor_min_waves(kCap)) void sensor_ke
     const uint32_t wv = threadIdx.x >> 6;
     const uint32_t lane = threadIdx.x & 63u;
     static_assert(kWaves % kSplit == 0, "split must divide the block's waves");
-    uint32_t w = blockIdx.x * (kWaves / kSplit) + wv / kSplit;
-    if (kSplit == 1 && S.sorder) {
-        // blocks in dispatch order take every tile's heaviest quad of worlds
-        // first, its lightest last (block b: tile b % ntiles, quad b / ntiles;
-        // used when every tile is full), so the kernel's drain runs the
-        // cheapest worlds and a block's four worlds cost about the same
+    constexpr uint32_t kWpb = kWaves / kSplit;   // worlds per block
+    uint32_t w = blockIdx.x * kWpb + wv / kSplit;
+    if (S.sorder) {
+        // blocks in dispatch order take every tile's heaviest worlds first,
+        // its lightest last (block b: tile b % ntiles, the tile's b / ntiles-th
+        // group of kWpb worlds; used when every tile is full), so the kernel's
+        // drain runs the cheapest worlds and a block's worlds cost about the same
         const uint32_t b = blockIdx.x, tile = b % S.ntiles, q = b / S.ntiles;
-        w = (uint32_t)S.sorder[(size_t)tile * kTileWorlds + q * kWaves + wv];
+        w = (uint32_t)S.sorder[(size_t)tile * kTileWorlds + q * kWpb + wv / kSplit];
     }
     w = uniform(w);
     constexpr int kChunkStep = kKeyAgents * kSplit;
@@ -1921,7 +1922,9 @@ bool sensor_order_used(uint32_t W)
 #ifdef MB_NO_SENSOR_ORDER
     return false;
 #else
-    return W > (uint32_t)MB_SENSOR_SPLIT_MAX && W % kTileWorlds == 0 && kSensorWorlds * 256 == kTileWorlds;
+    static_assert(kTileWorlds % kSensorWorlds == 0 && kTileWorlds % (MB_SENSOR_SPLIT_WAVES / MB_SENSOR_SPLIT) == 0,
+                  "a sensor block's worlds lie in one scan tile");
+    return W % kTileWorlds == 0;
 #endif
 }
 

@@ -38,7 +38,7 @@ struct SimState {
     float4 *raytab;                 // [36] per ray (32 pixels, the finder): u, NearPt c, s, e
     int32_t *sorder;                // [W] the sensor's world order (K2: each tile by descending
                                     // population), or null: world order (W not a multiple of
-                                    // the tile, or the split sensor)
+                                    // the 1024-world tile)
     // K1's output half of the double-buffered columns the sensor reads (the
     // sensor of step t runs beside step t+1's K1; swap_state after each K1)
     float *x_out, *y_out, *rw_out, *rz_out;
@@ -69,7 +69,7 @@ struct ObsTable {
 constexpr int kTotRows = 5;   // totals[kTotRows]: rows the moves / shift / checkpoints cover
 uint32_t scan_tiles(uint32_t W);
 // whether the sensor renders worlds in K2's population order (every scan tile
-// full and the one-wave-per-world sensor)
+// full)
 bool sensor_order_used(uint32_t W);
 // K1 blocks add their counts into one of kTileBuckets copies of their tile's
 // counters (block index mod 8): fewer same-address atomics at K1's end
