@@ -12,9 +12,10 @@ BASELINE config 3).  Rank 0 prints one JSON line.
     torchrun --nproc-per-node N bench.py --gpus N ...
 
 With several ranks (or --gather) a second timed loop measures BASELINE config
-5: after every step each rank's rollout records (the learner's raw columns,
-64 B/agent) are gathered to rank 0 over RCCL and the [N, 69] learner rows are
-rebuilt there (madrona-bots_amd/harness/gather.py); reported as "config5".
+5: after every step each rank's learner records (what the reference training
+loop reads, 272 B/agent) are gathered to rank 0 over RCCL and unpacked there,
+rank 0 picks actions and memory, and they are scattered back to the ranks that
+own the rows (madrona-bots_amd/harness/gather.py); reported as "config5".
 `python bench.py --gpus N` without a launcher starts the N ranks itself.
 
 After the main line (unless --no-secondary): the reference training loop's
@@ -65,15 +66,34 @@ LAZY_BYTES_PER_AGENT = 552.0 - 88.0
 LOOP_EXTRA_PER_AGENT = 2 * (84.0 + 276.0) + 16.0 + 88.0
 
 
+def cgroup_cpu_quota():
+    """CPUs of CPU time the process's cgroup grants per second (cgroup v2
+    cpu.max, or v1 cfs quota / period), or None when unlimited."""
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else int(q) / int(p)
+    except (OSError, ValueError):
+        pass
+    try:
+        q = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        p = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        return None if q <= 0 else q / p
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_share():
-    """Host CPUs this process may use: its affinity set, capped by the box's
-    per-GPU share (OMP_NUM_THREADS, 16 on the GPU box); and the machine's."""
+    """(effective CPUs, affinity CPUs, cgroup quota, machine CPUs): the
+    effective count is the affinity set capped by the cgroup's CPU quota --
+    what the process can actually run on at once (the affinity
+    mask alone overstated it)."""
     try:
         aff = len(os.sched_getaffinity(0))
     except AttributeError:
         aff = os.cpu_count() or 1
-    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
-    return (min(aff, omp) if omp > 0 else aff), aff, os.cpu_count()
+    quota = cgroup_cpu_quota()
+    eff = aff if quota is None else max(1, min(aff, int(quota + 0.5)))
+    return eff, aff, quota, os.cpu_count()
 
 
 def load_traffic(worlds):
@@ -145,9 +165,9 @@ def cpu_baseline(worlds_sample, target_s, threads=None):
     affinity set), on a bounded sample of the same workload (same seed,
     agents, action stream, step+shift+write)."""
     import madrona_bots as mb
-    share, aff, nproc = cpu_share()
+    eff, aff, quota, nproc = cpu_share()
     if threads is None:
-        threads = aff
+        threads = eff
     os.environ["MBOTS_CPU_THREADS"] = str(threads)
     sim = mb.SimManager(0, worlds_sample, SEED, AGENTS_PER_WORLD, exec_mode="cpu")
     sim.write_synthetic_actions(ACTION_SEED, 0)
@@ -164,7 +184,7 @@ def cpu_baseline(worlds_sample, target_s, threads=None):
         if dt >= target_s or steps >= 5000:
             break
     return {"value": (sim.agent_steps() - s0) / dt, "unit": "agent-steps/s", "cores": threads,
-            "nproc": nproc, "affinity_cpus": aff, "kind": "port",
+            "nproc": nproc, "affinity_cpus": aff, "cgroup_cpu_quota": quota, "kind": "port",
             "impl": "madrona_bots exec_mode='cpu' (madrona-bots_amd/csrc/mbots_cpu.cpp), "
                     "std::thread per world range",
             "sample": f"{worlds_sample} worlds x {AGENTS_PER_WORLD} agents, {steps} steps "
@@ -255,12 +275,8 @@ def spawn_ranks(args):
     --same-device)."""
     import socket
     import subprocess
-    if not args.same_device:
-        ndev = torch.cuda.device_count()   # counts devices without creating a HIP context
-        if ndev < args.gpus:
-            print(f"bench.py: --gpus {args.gpus} needs {args.gpus} devices, {ndev} visible "
-                  "(--same-device --backend gloo rehearses several ranks on one GPU)", file=sys.stderr)
-            return 2
+    # no GPU call here (not even a device count, which can fall back to
+    # hipGetDeviceCount): each rank checks that it has a device of its own
     with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
@@ -273,34 +289,49 @@ def spawn_ranks(args):
 
 
 def config5_loop(mgr, args, rank, world_size, dev, distributed):
-    """BASELINE config 5: every rank steps its shard; after each step the
-    learner's reads (learn/training_loop.py:43-57, :87) travel to rank 0 as
-    64-B rollout records (harness/gather.py gather_records: RCCL gather over
-    xGMI with the nccl backend), where the [N, 69] learner rows are rebuilt by
-    the construct_obs-equivalent kernel; then shift + the learner's action
-    write.  Wall clock of the timed steps, max over ranks; returns the line's
-    dict on rank 0."""
+    """BASELINE config 5: every rank steps its shard; after each step what the
+    learner reads (learn/training_loop.py:43-93: current and previous
+    observation columns, reward, stats, Action, HiddenState, PrevHiddenState)
+    travels to rank 0 as learner records (harness/gather.py gather_learner:
+    RCCL gather over xGMI with the nccl backend) and is unpacked there; rank 0
+    picks actions and memory (a stand-in for the PPO step, learn/models.py,
+    out of scope: random one-hot actions, memory from the gathered hidden
+    state); shift; the actions and memory go back to the ranks that own the
+    rows (scatter_actions, :136-137).  Wall clock of the timed steps, max over
+    ranks; returns the line's dict on rank 0."""
     import gather
     import madrona_bots as mb
     steps = max(10, args.steps // 2)
-    gsec = [0.0]
+    gsec = [0.0, 0.0]
     nrows = [0]
+    gen = torch.Generator(device=dev).manual_seed(ACTION_SEED)
 
     def one(t, timed):
         mgr.step()
         g0 = time.perf_counter()
         if distributed:
-            out = gather.gather_records(mgr, dst=0)
-        else:   # one rank: the same records, packed and rebuilt locally
-            out = mb.unpack_rollout(mgr.pack_rollout())
-        if out is not None:
-            nrows[0] += out["obs"].shape[0] if timed else 0
-        if timed:
-            gsec[0] += time.perf_counter() - g0
+            got, plan = gather.gather_learner(mgr, dst=0)
+        else:   # one rank: the same records, packed and unpacked locally
+            got, plan = mb.unpack_learner(mgr.pack_learner()), None
+        actions = memory = None
+        if got is not None:
+            n = got["obs"].shape[0]
+            nrows[0] += n if timed else 0
+            k = torch.randint(0, 6, (n,), device=dev, generator=gen)
+            actions = torch.nn.functional.one_hot(k, 6).to(torch.int32)
+            memory = got["hidden"] * 0.5 + got["obs"][:, :16] * (1.0 / 256.0)
+        g1 = time.perf_counter()
         mgr.shift_observations()
-        mgr.write_synthetic_actions(ACTION_SEED, t + 1)
+        if distributed:
+            gather.scatter_actions(mgr, actions, memory, plan, src=0)
+        else:
+            mgr.write_actions(actions, memory)
+        if timed:
+            gsec[0] += g1 - g0
+            gsec[1] += time.perf_counter() - g1
 
     t0s = args.warmup + args.steps + 100
+    mgr.write_synthetic_actions(ACTION_SEED, t0s, True)
     for k in range(3):
         one(t0s + k, False)
     torch.cuda.synchronize()
@@ -312,24 +343,25 @@ def config5_loop(mgr, args, rank, world_size, dev, distributed):
         one(t0s + 3 + k, True)
     torch.cuda.synchronize()
     el = time.perf_counter() - t0
-    st = torch.tensor([el, gsec[0]], dtype=torch.float64, device=dev if args.backend == "nccl" else "cpu")
+    st = torch.tensor([el, gsec[0], gsec[1]], dtype=torch.float64, device=dev if args.backend == "nccl" else "cpu")
     if distributed:
         dist.barrier()
         dist.all_reduce(st, op=dist.ReduceOp.MAX)
-    el, gs = float(st[0].item()), float(st[1].item())
+    el, gs, ss = (float(x) for x in st.tolist())
     if rank != 0:
         return None
     rows = nrows[0] / steps
-    rb = mgr.rollout_record_bytes()
-    return {"what": "step + rollout records (semantic, health, position, surrounding, reward, stats: "
-                    f"{rb} B/agent) gathered to rank 0 + [N,69] learner rows rebuilt there + shift + "
-                    "action write (harness/gather.py gather_records)",
-            "backend": args.backend if distributed else "none (one rank: pack + unpack locally)",
+    rb = mgr.learner_record_bytes()
+    return {"what": "step + learner records (current and previous observation columns, reward, stats, Action, "
+                    f"HiddenState, PrevHiddenState: {rb} B/agent) gathered to rank 0 and unpacked there + "
+                    "actions / memory chosen there + shift + actions / memory scattered back to the owning ranks "
+                    "(harness/gather.py gather_learner / scatter_actions)",
+            "backend": args.backend if distributed else "none (one rank: pack + unpack + write locally)",
             "n_gpus": world_size, "steps": steps, "ms_per_step": el / steps * 1e3,
-            "value": rows / (el / steps), "unit": "agent-steps/s (every rank's agents reaching the learner)",
-            "gather_ms_per_step": gs / steps * 1e3, "rows_per_step_at_learner": rows,
-            "gathered_bytes_per_step": rows * rb, "bytes_per_agent": rb,
-            "previous_payload_bytes_per_agent": 280}
+            "value": rows / (el / steps), "unit": "agent-steps/s (every rank's agents through the learner round trip)",
+            "gather_ms_per_step": gs / steps * 1e3, "scatter_ms_per_step": ss / steps * 1e3,
+            "rows_per_step_at_learner": rows,
+            "gathered_bytes_per_step": rows * rb, "scattered_bytes_per_step": rows * 88, "bytes_per_agent": rb}
 
 
 def main():
@@ -347,8 +379,8 @@ def main():
                     help="bracket every k-th timed step()+shift() with HIP events (roofline "
                          "launch duration); each event pair adds ~10 us of GPU idle")
     ap.add_argument("--gather", action="store_true",
-                    help="config 5 also at one rank (always run with several ranks): rollout records "
-                         "gathered to rank 0, learner rows rebuilt there")
+                    help="config 5 also at one rank (always run with several ranks): learner records "
+                         "gathered to rank 0, actions / memory scattered back")
     ap.add_argument("--backend", default="nccl",
                     help="torch.distributed backend for the bench's barrier/max/sum (nccl = RCCL); "
                          "gloo allows a rehearsal with several ranks on one GPU")
@@ -587,17 +619,11 @@ def main():
             out["secondary"] = secondary
             out["reference_loop"] = ref_main
         if not args.no_cpu_baseline:
-            # every CPU of the affinity set ("all host cores"), on a
-            # sample of >= 64 worlds per thread; beside it the box's per-GPU
-            # share (OMP_NUM_THREADS), the pool size the box asks workers to use
-            share, aff, _ = cpu_share()
-            base = cpu_baseline(max(args.cpu_worlds, 64 * aff), args.cpu_seconds / 2, threads=aff)
-            if share != aff:
-                sh = cpu_baseline(args.cpu_worlds, args.cpu_seconds / 2, threads=share)
-                base["per_gpu_share"] = {k: sh[k] for k in ("value", "cores", "sample")}
-                base["per_gpu_share"]["note"] = ("the box's per-GPU CPU share (OMP_NUM_THREADS); "
-                                                 "the headline value uses every CPU of the affinity set")
-            out["cpu_baseline"] = base
+            # every CPU the process can actually use ("all host
+            # cores"): its affinity set capped by the cgroup's CPU quota, one
+            # thread each, on a sample of >= 64 worlds per thread
+            eff = cpu_share()[0]
+            out["cpu_baseline"] = cpu_baseline(max(args.cpu_worlds, 64 * eff), args.cpu_seconds, threads=eff)
         print(json.dumps(out), flush=True)
 
     if distributed:

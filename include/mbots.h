@@ -127,8 +127,16 @@ int mbots_shift_observations(mbots_handle *h, void *stream);
 /* SimBridge::totalNumAgents (sim.hpp:74-78, sim.cpp:992-993).  Waits for the
  * last step's counters. */
 int mbots_num_agents(mbots_handle *h, uint32_t *out);
-/* Manager::exportTensor / the 11 tensor accessors (mgr.cpp:70-76, :199-422) */
+/* Manager::exportTensor / the 11 tensor accessors (mgr.cpp:70-76, :199-422).
+ * The reference's step() is synchronous (mgr.cpp:51-63), so its views are
+ * valid on any stream; mbots_export keeps that contract: it returns after the
+ * view's data is final (host-synchronising with the manager's last stream). */
 int mbots_export(mbots_handle *h, int32_t export_id, mbots_tensor *out);
+/* Stream-ordered form (what the Python surface uses): any deferred copy or
+ * join the view needs is enqueued on `stream`, after everything the manager
+ * enqueued on the stream of its previous call, so the view is final in
+ * stream order on `stream` (no host synchronisation). */
+int mbots_export_on(mbots_handle *h, int32_t export_id, void *stream, mbots_tensor *out);
 /* Manager::setAction (mgr.cpp:251-272): row = export row (species-major). */
 int mbots_set_action(mbots_handle *h, uint32_t row, const int32_t action[6]);
 /* Manager::agentOffsetForWorld (mgr.cpp:274-277) */
@@ -153,18 +161,64 @@ int mbots_construct_obs(mbots_handle *h, int32_t prev, float *out, uint64_t out_
  *         60..63  zero
  *         64..95  depth (uint8 x 32), only with MBOTS_FLAG_FIX_DEPTH_ALIAS
  * mbots_pack_rollout writes rows [0, min(N, out_rows)) into `out` (device
- * memory of the manager's GPU; host memory in CPU mode). */
+ * memory of the manager's GPU, 16-byte aligned; host memory in CPU mode). */
 #define MBOTS_ROLLOUT_BYTES        64u
 #define MBOTS_ROLLOUT_BYTES_DEPTH  96u
 int mbots_rollout_record_bytes(mbots_handle *h, uint32_t *out);
 int mbots_pack_rollout(mbots_handle *h, void *out, uint64_t out_rows, void *stream);
 /* Learner side, no manager needed: `rows` gathered records (with_depth: the
  * 96-B form) -> obs [rows, 69] f32 exactly as mbots_construct_obs builds them,
- * reward [rows] f32 and stats [rows, 4] int32 (either may be NULL; stats
- * 16-B aligned).  device >= 0: pointers are device memory of that GPU and the
+ * reward [rows] f32 and stats [rows, 4] int32 (either may be NULL; records
+ * and stats 16-B aligned on the device).  device >= 0: pointers are device memory of that GPU and the
  * kernel runs on `stream`; device == -1: host memory, done before returning. */
 int mbots_unpack_rollout(const void *records, uint64_t rows, int32_t with_depth, int32_t device,
                          float *obs, float *reward, int32_t *stats, void *stream);
+
+/* Learner records: the config-5 round trip (BASELINE config 5, SURVEY 8e
+ * steps 1-3).  Everything learn/training_loop.py reads between step() and its
+ * writes -- the rollout record above (current observation columns, reward,
+ * stats: :49-50, :58), the previous observation columns (:87), Action (:47,
+ * :93), HiddenState (:48, :58) and PrevHiddenState (:89) -- one record per
+ * export row:
+ *   bytes   0..63   the rollout record (bytes 60..63 zero)
+ *          64..95   prev semantic        96..99   prev health (int32 bits)
+ *         100..107  prev position       108..115  prev surrounding
+ *         116..139  Action (int32 x 6)  140..143  zero
+ *         144..207  HiddenState (f32 x 16)
+ *         208..271  PrevHiddenState (f32 x 16)
+ *         272..335  depth, prev depth (uint8 x 32 each), only with
+ *                   MBOTS_FLAG_FIX_DEPTH_ALIAS
+ * mbots_pack_learner writes rows [0, min(N, out_rows)) into `out` (16-byte
+ * aligned device memory; host memory in CPU mode). */
+#define MBOTS_LEARNER_BYTES        272u
+#define MBOTS_LEARNER_BYTES_DEPTH  336u
+int mbots_learner_record_bytes(mbots_handle *h, uint32_t *out);
+int mbots_pack_learner(mbots_handle *h, void *out, uint64_t out_rows, void *stream);
+/* Learner side (no manager): records -> any of these (NULL: skipped); obs and
+ * prev_obs are construct_obs rows of the current / previous columns
+ * (learn/util.py:14-29, bit-identical). */
+typedef struct mbots_learner_out {
+    float   *obs;          /* [rows, 69] */
+    float   *prev_obs;     /* [rows, 69] */
+    float   *reward;       /* [rows]     */
+    int32_t *stats;        /* [rows, 4]  */
+    int32_t *action;       /* [rows, 6]  */
+    float   *hidden;       /* [rows, 16] */
+    float   *prev_hidden;  /* [rows, 16] */
+} mbots_learner_out;
+int mbots_unpack_learner(const void *records, uint64_t rows, int32_t with_depth, int32_t device,
+                         const mbots_learner_out *out, void *stream);
+/* The learner's writes (training_loop.py:136-137: action_tensor[...] = one_hot,
+ * memory_tensor[...] = new_memory) for every row at once: `rows` rows of
+ * Action [rows, 6] int32 and/or HiddenState [rows, 16] f32 (either may be
+ * NULL) from memory of the manager's device (host memory in CPU mode) into
+ * the current export table, rows [0, rows).  rows is N, or mbots_num_rows()
+ * to also write the shard ghost's rows (the next shard's first world, which
+ * then acts exactly as on the next rank). */
+int mbots_write_actions(mbots_handle *h, const int32_t *action, const float *hidden, uint64_t rows,
+                        void *stream);
+/* every table row: N plus the shard ghost's (which follow row N) */
+int mbots_num_rows(mbots_handle *h, uint32_t *out);
 
 /* Checkpoint / restore (the reference has none): the live state
  * after the last step (agent SoA, RNG keys/counters, food, the current export
@@ -180,6 +234,9 @@ int mbots_load_checkpoint(mbots_handle *h, const void *host_src, uint64_t bytes)
 int mbots_world_state(mbots_handle *h, uint32_t world, float *xy_rwrz, int32_t *sp_hp_finder,
                       uint64_t *food, uint32_t *food_rot, int32_t *n_out);
 
+/* Stream ordering: every call that takes a stream enqueues on it after all
+ * work this manager enqueued on the stream of its previous call (an event
+ * hop when the two differ; not across a graph capture's boundary). */
 /* Build utilities (benchmark / test harness, not reference API):
  * identity-keyed synthetic action stream: one-hot(threefry(seed,step |
  * global_world, slot) % 6) written into the Action column of every live agent;

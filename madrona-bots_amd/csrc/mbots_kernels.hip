@@ -774,7 +774,9 @@ __global__ __launch_bounds__(256) void export_rows_kernel(SimState S, ObsTable n
         const float s0 = init ? 0.0f : S.sur0[base + i];
         const float s1 = init ? 0.0f : S.sur1[base + i];
         const uint32_t st = init ? 0u : S.stats[base + i];
-        S.src_of[r] = S.obsrow[base + i];
+        // old row: K1's obsrow_out (the sensor reads it beside this kernel);
+        // the new row goes to obsrow, which the next K1 reads
+        S.src_of[r] = S.obsrow_out[base + i];
         S.obsrow[base + i] = row;
         constexpr bool nt = (MB_NT & 4) != 0;
         st_stream(nxt.species + r, sp, nt);
@@ -1764,6 +1766,142 @@ __global__ __launch_bounds__(256) void unpack_rollout_kernel(const uint8_t *recs
 }
 
 // ---------------------------------------------------------------------------
+// Learner records (BASELINE config 5 round trip, include/mbots.h): everything
+// learn/training_loop.py reads between step() and its writes -- the rollout
+// record (current observation columns, reward, stats: :49-50, :58), the
+// previous observation columns (:87), Action (:47, :93), HiddenState (:48,
+// :58) and PrevHiddenState (:89) -- as one 272-B record per export row (336
+// with real depth).  The columns are read after the manager materialised the
+// step's deferred moves (`t` already holds each logical column's storage).
+// ---------------------------------------------------------------------------
+struct LearnerCols {
+    const int8_t *sem, *psem;
+    const uint8_t *depth, *pdepth;
+    const int32_t *health, *phealth, *stats, *action;
+    const float *pos, *ppos, *sur, *psur, *reward, *hidden, *phidden;
+};
+
+__global__ __launch_bounds__(256) void pack_learner_kernel(const uint32_t *totals, LearnerCols c, int fixd,
+                                                           uint8_t *out, uint32_t out_rows)
+{
+    const uint32_t N = min(totals[0], out_rows);
+    const uint32_t rec = fixd ? kLearnerBytesDepth : kLearnerBytes;
+    for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r < N; r += gridDim.x * blockDim.x) {
+        uint4 *o = reinterpret_cast<uint4 *>(out + (size_t)r * rec);
+        const uint4 *s = reinterpret_cast<const uint4 *>(c.sem + (size_t)r * kSensor);
+        const uint4 *ps = reinterpret_cast<const uint4 *>(c.psem + (size_t)r * kSensor);
+        o[0] = s[0];
+        o[1] = s[1];
+        const float2 p = reinterpret_cast<const float2 *>(c.pos)[r];
+        const float2 su = reinterpret_cast<const float2 *>(c.sur)[r];
+        const int4 st = reinterpret_cast<const int4 *>(c.stats)[r];
+        const uint32_t sb = (uint32_t)(st.x & 0xFF) | (uint32_t)(st.y & 0xFF) << 8 |
+                            (uint32_t)(st.z & 0xFF) << 16 | (uint32_t)(st.w & 0xFF) << 24;
+        o[2] = make_uint4((uint32_t)c.health[r], __float_as_uint(p.x), __float_as_uint(p.y), __float_as_uint(su.x));
+        o[3] = make_uint4(__float_as_uint(su.y), __float_as_uint(c.reward[r]), sb, 0u);
+        o[4] = ps[0];
+        o[5] = ps[1];
+        const float2 pp = reinterpret_cast<const float2 *>(c.ppos)[r];
+        const float2 psu = reinterpret_cast<const float2 *>(c.psur)[r];
+        const int2 *a = reinterpret_cast<const int2 *>(c.action + (size_t)r * 6);
+        const int2 a0 = a[0], a1 = a[1], a2 = a[2];
+        o[6] = make_uint4((uint32_t)c.phealth[r], __float_as_uint(pp.x), __float_as_uint(pp.y), __float_as_uint(psu.x));
+        o[7] = make_uint4(__float_as_uint(psu.y), (uint32_t)a0.x, (uint32_t)a0.y, (uint32_t)a1.x);
+        o[8] = make_uint4((uint32_t)a1.y, (uint32_t)a2.x, (uint32_t)a2.y, 0u);
+        const uint4 *hd = reinterpret_cast<const uint4 *>(c.hidden + (size_t)r * kHidden);
+        const uint4 *phd = reinterpret_cast<const uint4 *>(c.phidden + (size_t)r * kHidden);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) o[9 + k] = hd[k];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) o[13 + k] = phd[k];
+        if (fixd) {
+            const uint4 *d = reinterpret_cast<const uint4 *>(c.depth + (size_t)r * kSensor);
+            const uint4 *pd = reinterpret_cast<const uint4 *>(c.pdepth + (size_t)r * kSensor);
+            o[17] = d[0];
+            o[18] = d[1];
+            o[19] = pd[0];
+            o[20] = pd[1];
+        }
+    }
+}
+
+// Learner side: records -> obs / prev_obs [N, 69] (construct_obs of the
+// current / previous columns, bit-identical), reward [N], stats [N, 4],
+// action [N, 6], hidden / prev_hidden [N, 16]; any output but obs may be null.
+// 64 records per block staged in LDS, every output written as contiguous runs.
+__global__ __launch_bounds__(256) void unpack_learner_kernel(const uint8_t *recs, uint32_t N, int fixd,
+                                                             mbots_learner_out o)
+{
+    constexpr int kW = kLearnerBytesDepth / 16;   // granules per staged record (the widest)
+    __shared__ uint4 s_rec[kObsRows * kW];
+    const uint32_t rec = fixd ? kLearnerBytesDepth : kLearnerBytes, gpr = rec / 16;
+    const uint32_t nblk = (N + kObsRows - 1) / kObsRows;
+    const uint32_t t = threadIdx.x;
+    const uint8_t *sb = reinterpret_cast<const uint8_t *>(s_rec);
+    // obs column c of staged record r: the current (prev = 0) or previous part
+    auto val = [&](uint32_t i, int prev) {
+        const uint32_t r = i / kObsDim, c = i - r * kObsDim;
+        const uint8_t *q = sb + (size_t)r * kW * 16 + (prev ? 64 : 0);
+        const uint32_t *q32 = reinterpret_cast<const uint32_t *>(q);
+        if (c < 32) return (float)q[fixd ? (prev ? 240 : 272) + c : c];
+        if (c < 35) return __uint_as_float(q32[8 + (c - 32)]);
+        if (c < 67) return (float)(int8_t)q[c - 35];
+        return __uint_as_float(q32[11 + (c - 67)]);
+    };
+    auto word = [&](uint32_t r, uint32_t byte) {
+        return reinterpret_cast<const uint32_t *>(sb + (size_t)r * kW * 16 + byte)[0];
+    };
+    for (uint32_t b = blockIdx.x; b < nblk; b += gridDim.x) {
+        const uint32_t r0 = b * kObsRows, nr = min((uint32_t)kObsRows, N - r0);
+        for (uint32_t g = t; g < nr * gpr; g += 256) {
+            const uint32_t r = g / gpr, k = g - r * gpr;
+            s_rec[r * kW + k] = reinterpret_cast<const uint4 *>(recs + (size_t)r0 * rec)[g];
+        }
+        __syncthreads();
+#pragma unroll
+        for (int prev = 0; prev < 2; ++prev) {
+            float *out = prev ? o.prev_obs : o.obs;
+            if (!out) continue;
+            float *ob = out + (size_t)r0 * kObsDim;
+            if (nr == (uint32_t)kObsRows && (reinterpret_cast<uintptr_t>(out) & 15u) == 0) {
+                for (uint32_t g = t; g < kObsRows * kObsDim / 4; g += 256)
+                    st_stream(reinterpret_cast<uint4 *>(ob) + g,
+                              make_uint4(__float_as_uint(val(4 * g, prev)), __float_as_uint(val(4 * g + 1, prev)),
+                                         __float_as_uint(val(4 * g + 2, prev)),
+                                         __float_as_uint(val(4 * g + 3, prev))),
+                              MB_OBS_NT != 0);
+            } else {
+                for (uint32_t i = t; i < nr * kObsDim; i += 256) ob[i] = val(i, prev);
+            }
+        }
+        if (o.reward && t < nr) o.reward[r0 + t] = __uint_as_float(word(t, 52));
+        if (o.stats && t < nr) {
+            const uint32_t s4 = word(t, 56);
+            o.stats[4 * (size_t)(r0 + t) + 0] = (int32_t)(s4 & 0xFF);
+            o.stats[4 * (size_t)(r0 + t) + 1] = (int32_t)((s4 >> 8) & 0xFF);
+            o.stats[4 * (size_t)(r0 + t) + 2] = (int32_t)((s4 >> 16) & 0xFF);
+            o.stats[4 * (size_t)(r0 + t) + 3] = (int32_t)(s4 >> 24);
+        }
+        if (o.action)
+            for (uint32_t i = t; i < nr * 6; i += 256) {
+                const uint32_t r = i / 6, k = i - r * 6;
+                o.action[(size_t)r0 * 6 + i] = (int32_t)word(r, 116 + 4 * k);
+            }
+        if (o.hidden)
+            for (uint32_t i = t; i < nr * kHidden; i += 256) {
+                const uint32_t r = i / kHidden, k = i - r * kHidden;
+                o.hidden[(size_t)r0 * kHidden + i] = __uint_as_float(word(r, 144 + 4 * k));
+            }
+        if (o.prev_hidden)
+            for (uint32_t i = t; i < nr * kHidden; i += 256) {
+                const uint32_t r = i / kHidden, k = i - r * kHidden;
+                o.prev_hidden[(size_t)r0 * kHidden + i] = __uint_as_float(word(r, 208 + 4 * k));
+            }
+        __syncthreads();
+    }
+}
+
+// ---------------------------------------------------------------------------
 // K5: shiftObservationsSystem + shiftHiddenState (sim.cpp:1002-1048): Prev* <-
 // current for rows [0, N).  Each column is a contiguous byte range, so the copy
 // is one grid-stride stream of 16-byte granules over the concatenation of the
@@ -1835,6 +1973,7 @@ __global__ __launch_bounds__(256) void init_kernel(SimState S)
         S.health[base + i] = 100;
         S.finder[base + i] = -1;
         S.obsrow[base + i] = -1;
+        S.obsrow_out[base + i] = -1;   // the initial export's old rows: none
         S.sur0[base + i] = 0.0f;
         S.sur1[base + i] = 0.0f;
         S.stats[base + i] = 0u;
@@ -2057,8 +2196,10 @@ static void launch_sensor_cap(const SimState &S, const ObsTable &nxt, hipStream_
             MB_LAUNCH_EV((sensor_kernel<false, MB_SENSOR_SPLIT, kCap, kWv>), grid, blk, st, done, plain_events, S, nxt);
     } else {
         const dim3 grid((S.W + kSensorWorlds - 1) / kSensorWorlds), blk(64 * kSensorWorlds);
-        if (fixd) MB_LAUNCH_EV((sensor_kernel<true, 1, kCap, kSensorWorlds>), grid, blk, st, done, plain_events, S, nxt);
-        else MB_LAUNCH_EV((sensor_kernel<false, 1, kCap, kSensorWorlds>), grid, blk, st, done, plain_events, S, nxt);
+        if (fixd)
+            MB_LAUNCH_EV((sensor_kernel<true, 1, kCap, kSensorWorlds>), grid, blk, st, done, plain_events, S, nxt);
+        else
+            MB_LAUNCH_EV((sensor_kernel<false, 1, kCap, kSensorWorlds>), grid, blk, st, done, plain_events, S, nxt);
     }
 }
 hipError_t launch_sensor(const SimState &S, const ObsTable &nxt, hipStream_t st, hipEvent_t done,
@@ -2119,6 +2260,41 @@ hipError_t launch_unpack_rollout(const void *recs, uint32_t n, int fixd, float *
     const unsigned blocks = (unsigned)std::min<uint64_t>((n + kObsRows - 1) / kObsRows, 16384);
     hipLaunchKernelGGL(unpack_rollout_kernel, dim3(blocks), dim3(256), 0, st,
                        static_cast<const uint8_t *>(recs), n, fixd, obs, reward, stats);
+    return hipGetLastError();
+}
+hipError_t launch_pack_learner(const SimState &S, const ObsTable &t, int prev_lazy, void *out, uint32_t out_rows,
+                               hipStream_t st)
+{
+    const int fixd = (S.flags & kFlagFixDepth) != 0;
+    const bool lz = prev_lazy != 0;
+    LearnerCols c;
+    c.sem = t.sem;
+    c.psem = t.psem;
+    c.depth = t.depth;
+    c.pdepth = t.pdepth;
+    c.health = t.health;
+    c.phealth = lz ? t.health : t.phealth;
+    c.stats = t.stats;
+    c.action = t.action;
+    c.pos = t.pos;
+    c.ppos = lz ? t.pos : t.ppos;
+    c.sur = t.sur;
+    c.psur = lz ? t.sur : t.psur;
+    c.reward = t.reward;
+    c.hidden = t.hidden;
+    c.phidden = t.phidden;
+    const unsigned blocks = (unsigned)std::min<uint64_t>((out_rows + 255) / 256, 8192);
+    hipLaunchKernelGGL(pack_learner_kernel, dim3(std::max(blocks, 1u)), dim3(256), 0, st, S.totals, c, fixd,
+                       static_cast<uint8_t *>(out), out_rows);
+    return hipGetLastError();
+}
+hipError_t launch_unpack_learner(const void *recs, uint32_t n, int fixd, const mbots_learner_out &o,
+                                 hipStream_t st)
+{
+    if (n == 0) return hipSuccess;
+    const unsigned blocks = (unsigned)std::min<uint64_t>((n + kObsRows - 1) / kObsRows, 16384);
+    hipLaunchKernelGGL(unpack_learner_kernel, dim3(blocks), dim3(256), 0, st, static_cast<const uint8_t *>(recs), n,
+                       fixd, o);
     return hipGetLastError();
 }
 hipError_t launch_sensor_index(const SimState &S, int32_t *out, hipStream_t st)

@@ -2,6 +2,7 @@
 #pragma once
 
 #include "mbots_device.hpp"
+#include "../../include/mbots.h"
 
 namespace mbots {
 
@@ -15,7 +16,8 @@ struct SimState {
     int32_t *species;               // Species
     int32_t *health;                // Health (== HealthAccumulator between steps)
     int32_t *finder;                // FinderOutput hit -> slot in the same world, -1 none
-    int32_t *obsrow;                // AgentObservationBridge -> export row
+    int32_t *obsrow;                // AgentObservationBridge -> export row (K3a writes it, the
+                                    // next K1 reads it)
     float *sur0, *sur1;             // SurroundingObservation (step-local)
     uint32_t *stats;                // AgentStats bits (step-local)
     int32_t *n;                     // [W] live agents per world
@@ -42,7 +44,9 @@ struct SimState {
     // K1's output half of the double-buffered columns the sensor reads (the
     // sensor of step t runs beside step t+1's K1; swap_state after each K1)
     float *x_out, *y_out, *rw_out, *rz_out;
-    int32_t *species_out, *obsrow_out, *n_out;
+    int32_t *species_out, *n_out;
+    int32_t *obsrow_out;            // K1 -> K3a / the sensor: each slot's old export row (not
+                                    // swapped: K1 reads obsrow, K3a rewrites it)
     uint64_t *food_out;
     uint32_t W, cap, A, world_offset, flags, seed, ntiles;
     uint32_t Wx;                    // exported worlds: W, or W - 1 with the shard ghost (the
@@ -53,7 +57,7 @@ inline void swap_state(SimState &S)
 {
     auto sw = [](auto &a, auto &b) { auto t = a; a = b; b = t; };
     sw(S.x, S.x_out); sw(S.y, S.y_out); sw(S.rw, S.rw_out); sw(S.rz, S.rz_out);
-    sw(S.species, S.species_out); sw(S.obsrow, S.obsrow_out); sw(S.n, S.n_out);
+    sw(S.species, S.species_out); sw(S.n, S.n_out);
     sw(S.food, S.food_out);
 }
 
@@ -111,5 +115,13 @@ hipError_t launch_pack_rollout(const SimState &S, const ObsTable &t, void *out, 
                                hipStream_t st);
 hipError_t launch_unpack_rollout(const void *recs, uint32_t n, int fixd, float *obs, float *reward,
                                  int32_t *stats, hipStream_t st);
+// learner records of the config-5 round trip (MBOTS_LEARNER_BYTES[_DEPTH])
+constexpr uint32_t kLearnerBytes = 272, kLearnerBytesDepth = 336;
+// `t` holds every logical column's storage (the manager materialised the
+// step's deferred moves); prev_lazy: the six Prev* columns are the current ones
+hipError_t launch_pack_learner(const SimState &S, const ObsTable &t, int prev_lazy, void *out, uint32_t out_rows,
+                               hipStream_t st);
+hipError_t launch_unpack_learner(const void *recs, uint32_t n, int fixd, const mbots_learner_out &o,
+                                 hipStream_t st);
 
 }  // namespace mbots

@@ -99,6 +99,7 @@ struct mbots_handle {
     bool h_alias[2] = {false, false};
     bool prev_lazy[2] = {false, false};   // table half's six shift-owned Prev* columns are
                                           // still its current ones (lazy shift, K5)
+    hipEvent_t ev_hop = nullptr;      // orders a call's stream after the last one used
     int forced = 0;                   // deferred parts the caller's reads needed since the
                                       // last step (kMove*): the next step prefetches them
     int prefetched = 0;               // parts this step prefetched and no shift superseded
@@ -229,10 +230,32 @@ mbots::ObsTable src_view(const mbots_handle *h, int half)
     return t;
 }
 
-// make the caller's stream (the one step() ran on) wait for the sensor rows
-int wait_sensor(mbots_handle *h)
+// make `st` wait for the last step's sensor (its rows, and the moves it did)
+int wait_sensor(mbots_handle *h, hipStream_t st)
 {
-    if (h->last_join >= 0) HIP_TRY(hipStreamWaitEvent(h->last_stream, h->ev_join[h->last_join], 0));
+    if (h->last_join >= 0) HIP_TRY(hipStreamWaitEvent(st, h->ev_join[h->last_join], 0));
+    return MBOTS_OK;
+}
+
+bool capturing(hipStream_t st)
+{
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    return hipStreamIsCapturing(st, &cs) == hipSuccess && cs == hipStreamCaptureStatusActive;
+}
+
+// Every call enqueues on the caller's stream (torch's current stream); a call
+// on another stream than the previous one is ordered after everything the
+// manager enqueued there (an event hop), so steps, deferred copies and the
+// views they produce form one stream-ordered sequence whatever streams the
+// caller switches between.  (Not across a graph capture's boundary: a capture
+// cannot wait for work outside it.)
+int use_stream(mbots_handle *h, hipStream_t st)
+{
+    if (st != h->last_stream && !capturing(st) && !capturing(h->last_stream)) {
+        HIP_TRY(hipEventRecord(h->ev_hop, h->last_stream));
+        HIP_TRY(hipStreamWaitEvent(st, h->ev_hop, 0));
+    }
+    h->last_stream = st;
     return MBOTS_OK;
 }
 
@@ -262,9 +285,17 @@ int materialize_prev(mbots_handle *h, hipStream_t st)
 // the deferred K4 part: PrevAction / PrevHiddenState of the current half from
 // the other half, along the last step's src_of (both intact until the next
 // step's K3a / K4)
+int materialize_cur_ah(mbots_handle *h, hipStream_t st, int alias_cols);
 int materialize_prev_ah(mbots_handle *h, hipStream_t st)
 {
     if (!h->ah_pending[h->tb]) return MBOTS_OK;
+    // the Prev storage holds the current columns (aliased): copied out before
+    // the Prev move overwrites it
+    const int cols = (h->a_alias[h->tb] ? 1 : 0) | (h->h_alias[h->tb] ? 2 : 0);
+    if (cols) {
+        const int rc = materialize_cur_ah(h, st, cols);
+        if (rc) return rc;
+    }
     HIP_TRY(hipSetDevice(h->device));
     const int rc = timed(h, MBOTS_TK_MOVE, st, [&] {
         return mbots::launch_move(h->S, h->T[h->tb ^ 1], h->T[h->tb], 0, mbots::kMovePrevAH, st);
@@ -279,7 +310,7 @@ int materialize_prev_ah(mbots_handle *h, hipStream_t st)
 // columns of `alias_cols` (1 Action, 2 HiddenState) a fused shift left as
 // views of their Prev columns are copied out
 int sync_totals(mbots_handle *h);
-int materialize_cur_ah(mbots_handle *h, hipStream_t st, int alias_cols = 3)
+int materialize_cur_ah(mbots_handle *h, hipStream_t st, int alias_cols)
 {
     const int tb = h->tb;
     if (h->cur_ah_pending[tb]) {
@@ -378,7 +409,9 @@ struct CkptHeader {
     uint32_t version, num_worlds, cap, A, world_offset, flags, seed, n_rows;
     uint64_t bytes;
 };
-constexpr uint32_t kCkptVersion = 2;
+// 3: totals[kTotRows] (every table row, the shard ghost's included) is part
+// of the state and must equal the header's n_rows
+constexpr uint32_t kCkptVersion = 3;
 
 struct Seg {
     void *p;
@@ -451,6 +484,56 @@ void unpack_rollout_host(const uint8_t *recs, uint64_t n, bool with_depth, float
         if (reward) memcpy(reward + r, q + 52, 4);
         if (stats)
             for (int k = 0; k < 4; ++k) stats[4 * r + k] = q[56 + k];
+    }
+}
+
+// learner records on the host (CPU mode, and a gather that landed in host
+// memory): the layout of include/mbots.h, the values of pack_learner_kernel /
+// unpack_learner_kernel
+void pack_learner_host(const mbots::cpu::Table &t, bool fixd, uint64_t n, uint8_t *out)
+{
+    const size_t rec = fixd ? MBOTS_LEARNER_BYTES_DEPTH : MBOTS_LEARNER_BYTES;
+    for (uint64_t r = 0; r < n; ++r) {
+        uint8_t *o = out + r * rec;
+        pack_rollout_host(t.sem.data() + r * mbots::kSensor, nullptr, t.health.data() + r, t.pos.data() + 2 * r,
+                          t.sur.data() + 2 * r, t.reward.data() + r, t.stats.data() + 4 * r, 1, o);
+        memcpy(o + 64, t.psem.data() + r * mbots::kSensor, 32);
+        memcpy(o + 96, t.phealth.data() + r, 4);
+        memcpy(o + 100, t.ppos.data() + 2 * r, 8);
+        memcpy(o + 108, t.psur.data() + 2 * r, 8);
+        memcpy(o + 116, t.action.data() + 6 * r, 24);
+        memset(o + 140, 0, 4);
+        memcpy(o + 144, t.hidden.data() + mbots::kHidden * r, 64);
+        memcpy(o + 208, t.phidden.data() + mbots::kHidden * r, 64);
+        if (fixd) {
+            memcpy(o + 272, t.depth.data() + r * mbots::kSensor, 32);
+            memcpy(o + 304, t.pdepth.data() + r * mbots::kSensor, 32);
+        }
+    }
+}
+
+void unpack_learner_host(const uint8_t *recs, uint64_t n, bool fixd, const mbots_learner_out &o)
+{
+    const size_t rec = fixd ? MBOTS_LEARNER_BYTES_DEPTH : MBOTS_LEARNER_BYTES;
+    for (uint64_t r = 0; r < n; ++r) {
+        const uint8_t *q = recs + r * rec;
+        for (int prev = 0; prev < 2; ++prev) {
+            float *ob = prev ? o.prev_obs : o.obs;
+            if (!ob) continue;
+            ob += r * 69;
+            const uint8_t *b = q + (prev ? 64 : 0);
+            const uint8_t *d = fixd ? q + (prev ? 304 : 272) : b;
+            for (int c = 0; c < 32; ++c) ob[c] = (float)d[c];
+            memcpy(ob + 32, b + 32, 12);   // health bits, position
+            for (int c = 0; c < 32; ++c) ob[35 + c] = (float)(int8_t)b[c];
+            memcpy(ob + 67, b + 44, 8);    // surroundings
+        }
+        if (o.reward) memcpy(o.reward + r, q + 52, 4);
+        if (o.stats)
+            for (int k = 0; k < 4; ++k) o.stats[4 * r + k] = q[56 + k];
+        if (o.action) memcpy(o.action + 6 * r, q + 116, 24);
+        if (o.hidden) memcpy(o.hidden + mbots::kHidden * r, q + 144, 64);
+        if (o.prev_hidden) memcpy(o.prev_hidden + mbots::kHidden * r, q + 208, 64);
     }
 }
 
@@ -538,6 +621,7 @@ int mbots_create(const mbots_config *cfg_in, mbots_handle **out)
     // pinned row counts, which K2 writes system-coherent and fences itself)
     constexpr unsigned kSyncEvent = hipEventDisableTiming | hipEventReleaseToDevice;
     check(hipEventCreateWithFlags(&h->ev_totals, kSyncEvent), "hipEventCreateWithFlags");
+    check(hipEventCreateWithFlags(&h->ev_hop, kSyncEvent), "hipEventCreateWithFlags");
     check(hipEventCreateWithFlags(&h->ev_join[0], kSyncEvent), "hipEventCreateWithFlags");
     check(hipEventCreateWithFlags(&h->ev_join[1], kSyncEvent), "hipEventCreateWithFlags");
     {
@@ -585,6 +669,7 @@ int mbots_destroy(mbots_handle *h)
     for (auto &p : h->pending) { (void)hipEventDestroy(p.a); (void)hipEventDestroy(p.b); }
     for (auto e : h->pool) (void)hipEventDestroy(e);
     if (h->ev_totals) (void)hipEventDestroy(h->ev_totals);
+    if (h->ev_hop) (void)hipEventDestroy(h->ev_hop);
     for (auto e : h->ev_join) if (e) (void)hipEventDestroy(e);
     if (h->aux) (void)hipStreamDestroy(h->aux);
     if (h->h_totals) (void)hipHostFree(h->h_totals);
@@ -602,34 +687,7 @@ int mbots_step(mbots_handle *h, void *stream)
     }
     HIP_TRY(hipSetDevice(h->device));
     hipStream_t st = as_stream(stream);
-    h->last_stream = st;
-    // K1 reads the learner's actions through the half's view (an aliased
-    // Action column is its PrevAction), and so do this step's moves
-    const mbots::ObsTable cur = src_view(h, h->tb);
-    const mbots::ObsTable &nxt = h->T[h->tb ^ 1];
     int rc;
-    const int par = h->parity;
-    const int lazy = h->prev_lazy[h->tb] ? 1 : 0;
-    // the parts the caller's reads forced last step (a learner that reads the
-    // observation and PrevHiddenState between step and shift, as
-    // training_loop.py:47-88 does): moved right after this step's K3a, beside
-    // the sensor, instead of behind the wait for it (DESIGN.md "Prefetch")
-#ifdef MB_NO_FORK
-    const int prefetch = h->forced & ~mbots::kMoveSensor;
-#else
-    const int prefetch = h->forced;
-#endif
-    h->forced = 0;
-    h->prefetched = prefetch;
-    // no shift since the last step: its deferred Prev moves first
-    if (h->six_pending[h->tb] && (rc = materialize_prev(h, st))) return rc;
-    if ((rc = materialize_prev_ah(h, st))) return rc;
-    if ((rc = materialize_cur_ah(h, st, 0))) return rc;
-    if ((rc = materialize_psem(h, st))) return rc;   // before this step's sensor rewrites its source
-    // K1 reads the finder slots the previous step's sensor wrote, and writes the
-    // state half that sensor read; the halves swap after K1.
-    // (under stream capture only a join recorded in the same capture is waited
-    // for: a replay starts after the previous launch of the graph completed)
     hipStreamCaptureStatus cap_status = hipStreamCaptureStatusNone;
     unsigned long long cap_id = 0;
     HIP_TRY(hipStreamGetCaptureInfo(st, &cap_status, &cap_id));
@@ -637,20 +695,43 @@ int mbots_step(mbots_handle *h, void *stream)
     if (capturing) {
         if (cap_id != h->cap_seen) { h->cap_seen = cap_id; h->cap_steps = 0; }
         ++h->cap_steps;
+    } else if (h->cap_steps & 1) {
+        // a graph that ended without mbots_join holds an odd number of steps:
+        // every replay would leave the table halves and this bookkeeping out of
+        // step with the device
+        h->cap_steps = 0;
+        return fail(MBOTS_E_INVALID, "the last graph capture recorded an odd number of steps; "
+                                     "capture an even number (and end it with join())");
     }
-#ifndef MB_PROBE_NO_JOIN   // (timing probe only: K1 overwrites the state the sensor reads)
+    if ((rc = use_stream(h, st))) return rc;
+    const mbots::ObsTable &nxt = h->T[h->tb ^ 1];
+    const int par = h->parity;
+    const int lazy = h->prev_lazy[h->tb] ? 1 : 0;
+    // the parts the caller's reads forced last step (a learner that reads the
+    // observation and PrevHiddenState between step and shift, as
+    // training_loop.py:47-88 does): moved right after this step's K3a, beside
+    // the sensor, instead of behind the wait for it (DESIGN.md "Prefetch")
+    const int prefetch = h->forced;
+    h->forced = 0;
+    h->prefetched = prefetch;
+    // no shift since the last step: its deferred Prev moves first
+    if (h->six_pending[h->tb] && (rc = materialize_prev(h, st))) return rc;
+    if ((rc = materialize_prev_ah(h, st))) return rc;
+    if ((rc = materialize_cur_ah(h, st, 0))) return rc;
+    if ((rc = materialize_psem(h, st))) return rc;   // before this step's sensor rewrites its source
+    // K1 reads the learner's actions through the half's view (an aliased
+    // Action column is its PrevAction), and so do this step's moves
+    const mbots::ObsTable cur = src_view(h, h->tb);
+    // K1 reads the finder slots the previous step's sensor wrote, and writes the
+    // state half that sensor read; the halves swap after K1.
+    // (under stream capture only a join recorded in the same capture is waited
+    // for: a replay starts after the previous launch of the graph completed)
     if (h->last_join >= 0 && (!capturing || h->join_capture == cap_id))
         HIP_TRY(hipStreamWaitEvent(st, h->ev_join[h->last_join], 0));
-#endif
     if ((rc = timed(h, MBOTS_TK_WORLD_STEP, st,
                     [&] { return mbots::launch_world_step(h->S, cur, par, st); })))
         return rc;
     mbots::swap_state(h->S);
-#ifdef MB_PROBE_FORK_K1   // (timing probe only: the sensor reads a stale row_base -- wrong rows)
-    static hipEvent_t ev_k1 = nullptr;
-    if (!ev_k1) HIP_TRY(hipEventCreateWithFlags(&ev_k1, hipEventDisableTiming));
-    HIP_TRY(hipEventRecord(ev_k1, st));
-#endif
     // K2 writes the row counts into the pinned mirror; accessors and the
     // sensor's stream wait on ev_totals, carried by K2's own dispatch
     // (under stream capture -- a caller recording steps into a HIP graph -- the
@@ -658,36 +739,22 @@ int mbots_step(mbots_handle *h, void *stream)
     if ((rc = timed(h, MBOTS_TK_SCAN, st,
                     [&] { return mbots::launch_scan(h->S, par, st, h->ev_totals, capturing); })))
         return rc;
-#ifdef MB_NO_FORK
-    if ((rc = timed(h, MBOTS_TK_EXPORT, st,
-                    [&] { return mbots::launch_export_rows(h->S, nxt, 0, st); })))
-        return rc;
-    if ((rc = timed(h, MBOTS_TK_MOVE, st,
-                    [&] { return mbots::launch_move(h->S, cur, nxt, lazy, mbots::kMoveSensor, st); })))
-        return rc;
-    if ((rc = timed(h, MBOTS_TK_SENSOR, st, [&] { return mbots::launch_sensor(h->S, nxt, st); })))
-        return rc;
-#else
     // fork after K2: the K3b sensor (VALU-bound; it derives the export rows from
     // K2's row_base itself) runs on the aux stream while this stream goes on
-    // with K3a export, K4 move, shift_observations and the learner's action
-    // writes -- none of which reads the sensor rows or the finder slots.  The
-    // next step's K1 and the semantic/depth accessors wait for ev_join.
+    // with K3a export, shift_observations and the learner's action writes --
+    // none of which reads the sensor rows or the finder slots.  The next step's
+    // K1 and the semantic/depth accessors wait for ev_join.
     const int jcur = h->last_join == 0 ? 1 : 0;
-#ifdef MB_PROBE_FORK_K1
-    HIP_TRY(hipStreamWaitEvent(h->aux, ev_k1, 0));
-#else
     HIP_TRY(hipStreamWaitEvent(h->aux, h->ev_totals, 0));
-#endif
-    if ((rc = timed(h, MBOTS_TK_SENSOR, h->aux,
-                    [&] { return mbots::launch_sensor(h->S, nxt, h->aux, h->ev_join[jcur], capturing); })))
+    if ((rc = timed(h, MBOTS_TK_SENSOR, h->aux, [&] {
+             return mbots::launch_sensor(h->S, nxt, h->aux, h->ev_join[jcur], capturing);
+         })))
         return rc;
     h->last_join = jcur;
     h->join_capture = capturing ? cap_id : 0;
     if ((rc = timed(h, MBOTS_TK_EXPORT, st,
                     [&] { return mbots::launch_export_rows(h->S, nxt, 0, st); })))
         return rc;
-#endif
     if (prefetch && (rc = timed(h, MBOTS_TK_MOVE, st, [&] {
                          return mbots::launch_move(h->S, cur, nxt, lazy, prefetch, st);
                      })))
@@ -695,20 +762,19 @@ int mbots_step(mbots_handle *h, void *stream)
     ++h->steps;
     h->parity ^= 1;
     h->tb ^= 1;
+    const int nt = h->tb;
     // the new half's Prev* columns: eight moves deferred (a shift overwrites them)
-    h->prev_lazy[h->tb] = false;
-    h->a_alias[h->tb] = h->h_alias[h->tb] = false;
-    h->cur_ah_pending[h->tb] = true;
-#ifndef MB_NO_FORK
-    h->psem_pending[h->tb] = true;
-#endif
-    h->ah_pending[h->tb] = true;
-    h->six_pending[h->tb] = true;
-    h->six_lazy[h->tb] = lazy != 0;
-    if (prefetch & mbots::kMoveAH) h->cur_ah_pending[h->tb] = false;
-    if (prefetch & mbots::kMoveSensor) h->psem_pending[h->tb] = false;
-    if (prefetch & mbots::kMovePrevAH) h->ah_pending[h->tb] = false;
-    if (prefetch & mbots::kMovePrev6) h->six_pending[h->tb] = false;
+    h->prev_lazy[nt] = false;
+    h->a_alias[nt] = h->h_alias[nt] = false;
+    h->cur_ah_pending[nt] = true;
+    h->psem_pending[nt] = true;
+    h->ah_pending[nt] = true;
+    h->six_pending[nt] = true;
+    h->six_lazy[nt] = lazy != 0;
+    if (prefetch & mbots::kMoveAH) h->cur_ah_pending[nt] = false;
+    if (prefetch & mbots::kMoveSensor) h->psem_pending[nt] = false;
+    if (prefetch & mbots::kMovePrevAH) h->ah_pending[nt] = false;
+    if (prefetch & mbots::kMovePrev6) h->six_pending[nt] = false;
     return MBOTS_OK;
 }
 
@@ -721,18 +787,17 @@ int mbots_shift_observations(mbots_handle *h, void *stream)
     }
     HIP_TRY(hipSetDevice(h->device));
     hipStream_t st = as_stream(stream);
-    h->last_stream = st;
+    int rc = use_stream(h, st);
+    if (rc) return rc;
     // Action / HiddenState now; the other six Prev* columns stay views of the
     // current ones until the next step or an accessor needs them (K5, lazy
-    // shift).  Action / HiddenState still in the other half: one gather writes
-    // their Prev copies, and the current columns become views of those (the
-    // learner overwrites them next; DESIGN.md "Aliased current Action /
-    // HiddenState") -- the fused shift; the prev sensor rides along when still
-    // pending.
+    // shift).  Action / HiddenState still in the other half: one gather writes their
+    // Prev copies, and the current columns become views of those (the learner
+    // overwrites them next; DESIGN.md "Aliased current Action / HiddenState")
+    // -- the fused shift; the prev sensor rides along when still pending.
     const int tb = h->tb;
     const bool fused = h->cur_ah_pending[tb];
     const bool with_psem = fused && h->psem_pending[tb];
-    int rc = MBOTS_OK;
     if (fused) {
         const mbots::ObsTable src = src_view(h, tb ^ 1);
         rc = timed(h, MBOTS_TK_SHIFT, st, [&] {
@@ -740,7 +805,7 @@ int mbots_shift_observations(mbots_handle *h, void *stream)
                                       mbots::kMoveAHShift | (with_psem ? mbots::kMoveSensor : 0), st);
         });
     } else if (!(h->a_alias[tb] && h->h_alias[tb])) {   // both aliased: already equal
-        if ((rc = materialize_cur_ah(h, st))) return rc;
+        if ((rc = materialize_cur_ah(h, st, 3))) return rc;
         rc = timed(h, MBOTS_TK_SHIFT, st,
                    [&] { return mbots::launch_shift(h->S, h->T[tb], mbots::kShiftEager, st); });
     }
@@ -771,7 +836,7 @@ int mbots_num_agents(mbots_handle *h, uint32_t *out)
     return MBOTS_OK;
 }
 
-int mbots_export(mbots_handle *h, int32_t id, mbots_tensor *out)
+int mbots_export_on(mbots_handle *h, int32_t id, void *stream, mbots_tensor *out)
 {
     using namespace mbots;
     if (!h || !out) return fail(MBOTS_E_INVALID, "null argument");
@@ -779,28 +844,33 @@ int mbots_export(mbots_handle *h, int32_t id, mbots_tensor *out)
         const int r = h->cpu->export_tensor(id, out);
         return r ? fail(r, "unknown export id " + std::to_string(id)) : MBOTS_OK;
     }
+    HIP_TRY(hipSetDevice(h->device));
+    hipStream_t st = as_stream(stream);
     uint32_t N = 0;
     int rc = mbots_num_agents(h, &N);
     if (rc) return rc;
+    // the view's deferred copies and joins go on the reader's stream, after
+    // everything the manager enqueued (the step may have run on another)
+    if ((rc = use_stream(h, st))) return rc;
     const int owed = pending_mask(h);
     int need = 0;
     switch (id) {
     case MBOTS_EXPORT_PREV_SPECIES: case MBOTS_EXPORT_PREV_POSITION: case MBOTS_EXPORT_PREV_HEALTH:
     case MBOTS_EXPORT_PREV_SURROUNDING: case MBOTS_EXPORT_PREV_REWARD: case MBOTS_EXPORT_PREV_STATS:
         need = mbots::kMovePrev6;
-        if ((rc = materialize_prev(h, h->last_stream))) return rc;
+        if ((rc = materialize_prev(h, st))) return rc;
         break;
     case MBOTS_EXPORT_PREV_ACTION: case MBOTS_EXPORT_PREV_HIDDEN_STATE:
         need = mbots::kMovePrevAH;
-        if ((rc = materialize_prev_ah(h, h->last_stream))) return rc;
+        if ((rc = materialize_prev_ah(h, st))) return rc;
         break;
     case MBOTS_EXPORT_ACTION: case MBOTS_EXPORT_HIDDEN_STATE:
         need = mbots::kMoveAH;
-        if ((rc = materialize_cur_ah(h, h->last_stream, id == MBOTS_EXPORT_ACTION ? 1 : 2))) return rc;
+        if ((rc = materialize_cur_ah(h, st, id == MBOTS_EXPORT_ACTION ? 1 : 2))) return rc;
         break;
     case MBOTS_EXPORT_PREV_SENSOR_SEMANTIC: case MBOTS_EXPORT_PREV_SENSOR_DEPTH:
         need = mbots::kMoveSensor;
-        if ((rc = materialize_psem(h, h->last_stream))) return rc;
+        if ((rc = materialize_psem(h, st))) return rc;
         break;
     default: break;
     }
@@ -827,11 +897,11 @@ int mbots_export(mbots_handle *h, int32_t id, mbots_tensor *out)
     case MBOTS_EXPORT_SURROUNDING: p = t.sur; dt = MBOTS_DTYPE_FLOAT32; cols = 2; break;
     case MBOTS_EXPORT_PREV_SURROUNDING: p = t.psur; dt = MBOTS_DTYPE_FLOAT32; cols = 2; break;
     case MBOTS_EXPORT_SENSOR_SEMANTIC:
-        if ((rc = wait_sensor(h))) return rc;
+        if ((rc = wait_sensor(h, st))) return rc;
         p = t.sem; dt = MBOTS_DTYPE_INT8; cols = kSensor; break;
     // SensorDepth exports the semantic buffer (sim.cpp:102-104, B.1) unless fixed
     case MBOTS_EXPORT_SENSOR_DEPTH:
-        if ((rc = wait_sensor(h))) return rc;
+        if ((rc = wait_sensor(h, st))) return rc;
         p = fixd ? (void *)t.depth : (void *)t.sem; dt = MBOTS_DTYPE_UINT8; cols = kSensor; break;
     case MBOTS_EXPORT_PREV_SENSOR_SEMANTIC: p = t.psem; dt = MBOTS_DTYPE_INT8; cols = kSensor; break;
     case MBOTS_EXPORT_PREV_SENSOR_DEPTH:
@@ -839,7 +909,6 @@ int mbots_export(mbots_handle *h, int32_t id, mbots_tensor *out)
     case MBOTS_EXPORT_STATS: p = t.stats; cols = 4; break;
     case MBOTS_EXPORT_PREV_STATS: p = t.pstats; cols = 4; break;
     case MBOTS_EXPORT_SENSOR_INDEX: {
-        hipStream_t st = h->last_stream;
         HIP_TRY(mbots::launch_sensor_index(h->S, h->sensor_index, st));
         HIP_TRY(hipStreamSynchronize(st));
         p = h->sensor_index;
@@ -858,6 +927,18 @@ int mbots_export(mbots_handle *h, int32_t id, mbots_tensor *out)
     return MBOTS_OK;
 }
 
+int mbots_export(mbots_handle *h, int32_t id, mbots_tensor *out)
+{
+    if (!h || !out) return fail(MBOTS_E_INVALID, "null argument");
+    if (h->cpu) return mbots_export_on(h, id, nullptr, out);
+    // the reference's views are valid on any stream once the synchronous
+    // step() returned (mgr.cpp:51-63): so are these, once this returns
+    const int rc = mbots_export_on(h, id, h->last_stream, out);
+    if (rc) return rc;
+    if (!capturing(h->last_stream)) HIP_TRY(hipStreamSynchronize(h->last_stream));
+    return MBOTS_OK;
+}
+
 int mbots_set_action(mbots_handle *h, uint32_t row, const int32_t action[6])
 {
     if (!h || !action) return fail(MBOTS_E_INVALID, "null argument");
@@ -869,12 +950,14 @@ int mbots_set_action(mbots_handle *h, uint32_t row, const int32_t action[6])
         memcpy(&h->cpu->table().action[(size_t)row * 6], action, 6 * sizeof(int32_t));
         return MBOTS_OK;
     }
+    HIP_TRY(hipSetDevice(h->device));
     const int owed = pending_mask(h);
-    if ((rc = materialize_cur_ah(h, h->last_stream, 1))) return rc;
+    hipStream_t st = h->last_stream;
+    if ((rc = materialize_cur_ah(h, st, 1))) return rc;
     note_use(h, mbots::kMoveAH, owed);
     HIP_TRY(hipMemcpyAsync(h->T[h->tb].action + (size_t)row * 6, action, 6 * sizeof(int32_t),
-                           hipMemcpyHostToDevice, h->last_stream));
-    HIP_TRY(hipStreamSynchronize(h->last_stream));
+                           hipMemcpyHostToDevice, st));
+    HIP_TRY(hipStreamSynchronize(st));
     return MBOTS_OK;
 }
 
@@ -904,12 +987,12 @@ int mbots_write_synthetic_actions(mbots_handle *h, uint32_t seed, uint32_t step,
     }
     HIP_TRY(hipSetDevice(h->device));
     hipStream_t st = as_stream(stream);
-    h->last_stream = st;
+    int rc = use_stream(h, st);
+    if (rc) return rc;
     const int owed = pending_mask(h);
     // the writer rewrites every live row's Action (and HiddenState with
     // write_hidden): an aliased column of those is simply written, not copied
-    int rc = materialize_cur_ah(h, st, 0);
-    if (rc) return rc;
+    if ((rc = materialize_cur_ah(h, st, 0))) return rc;
     note_use(h, mbots::kMoveAH, owed);
     rc = timed(h, MBOTS_TK_ACTIONS, st, [&] {
         return mbots::launch_synthetic_actions(h->S, h->T[h->tb], seed, step, write_hidden, st);
@@ -930,10 +1013,10 @@ int mbots_construct_obs(mbots_handle *h, int32_t prev, float *out, uint64_t out_
     }
     HIP_TRY(hipSetDevice(h->device));
     hipStream_t st = as_stream(stream);
-    h->last_stream = st;
-    int rc;
+    int rc = use_stream(h, st);
+    if (rc) return rc;
     const int owed = pending_mask(h);
-    if (!prev && (rc = wait_sensor(h))) return rc;   // current semantic rows come from K3b
+    if (!prev && (rc = wait_sensor(h, st))) return rc;   // current semantic rows come from K3b
     // The previous rows' health / position / surrounding: while the step's
     // deferred move of the six Prev* columns is still owed, gathered from the
     // other half along src_of inside this launch (what the move would write,
@@ -969,14 +1052,115 @@ int mbots_pack_rollout(mbots_handle *h, void *out, uint64_t out_rows, void *stre
                           t.sur.data(), t.reward.data(), t.stats.data(), n, static_cast<uint8_t *>(out));
         return MBOTS_OK;
     }
+    if ((reinterpret_cast<uintptr_t>(out) & 15u) != 0) return fail(MBOTS_E_INVALID, "out must be 16-byte aligned");
     HIP_TRY(hipSetDevice(h->device));
     hipStream_t st = as_stream(stream);
-    h->last_stream = st;
-    int rc = wait_sensor(h);   // the semantic / depth rows come from K3b
+    int rc = use_stream(h, st);
     if (rc) return rc;
+    if ((rc = wait_sensor(h, st))) return rc;   // the semantic / depth rows come from K3b
     return timed(h, MBOTS_TK_OBS, st, [&] {
         return mbots::launch_pack_rollout(h->S, h->T[h->tb], out, (uint32_t)out_rows, st);
     });
+}
+
+int mbots_learner_record_bytes(mbots_handle *h, uint32_t *out)
+{
+    if (!h || !out) return fail(MBOTS_E_INVALID, "null argument");
+    *out = (h->cfg.flags & MBOTS_FLAG_FIX_DEPTH_ALIAS) ? MBOTS_LEARNER_BYTES_DEPTH : MBOTS_LEARNER_BYTES;
+    return MBOTS_OK;
+}
+
+int mbots_pack_learner(mbots_handle *h, void *out, uint64_t out_rows, void *stream)
+{
+    if (!h || !out) return fail(MBOTS_E_INVALID, "null argument");
+    if (out_rows > 0xFFFFFFFFull) return fail(MBOTS_E_INVALID, "out_rows too large");
+    const bool fixd = (h->cfg.flags & MBOTS_FLAG_FIX_DEPTH_ALIAS) != 0;
+    if (h->cpu) {
+        pack_learner_host(h->cpu->table(), fixd, std::min<uint64_t>(h->cpu->num_agents(), out_rows),
+                          static_cast<uint8_t *>(out));
+        return MBOTS_OK;
+    }
+    if ((reinterpret_cast<uintptr_t>(out) & 15u) != 0) return fail(MBOTS_E_INVALID, "out must be 16-byte aligned");
+    HIP_TRY(hipSetDevice(h->device));
+    hipStream_t st = as_stream(stream);
+    int rc = use_stream(h, st);
+    if (rc) return rc;
+    // every column the record carries in its storage: the step's deferred
+    // moves the learner's reads need (and remembered, like the accessors', so
+    // the next step prefetches them beside its sensor)
+    const int owed = pending_mask(h);
+    if ((rc = materialize_prev(h, st))) return rc;
+    if ((rc = materialize_prev_ah(h, st))) return rc;
+    if ((rc = materialize_cur_ah(h, st, 3))) return rc;
+    if ((rc = materialize_psem(h, st))) return rc;
+    note_use(h, mbots::kMovePrev6 | mbots::kMovePrevAH | mbots::kMoveAH | mbots::kMoveSensor, owed);
+    if ((rc = wait_sensor(h, st))) return rc;   // the sensor rows (and what it moved)
+    return timed(h, MBOTS_TK_OBS, st, [&] {
+        return mbots::launch_pack_learner(h->S, h->T[h->tb], h->prev_lazy[h->tb] ? 1 : 0, out, (uint32_t)out_rows,
+                                          st);
+    });
+}
+
+int mbots_unpack_learner(const void *records, uint64_t rows, int32_t with_depth, int32_t device,
+                         const mbots_learner_out *out, void *stream)
+{
+    if (!out || (!records && rows)) return fail(MBOTS_E_INVALID, "null argument");
+    if (rows > 0xFFFFFFFFull) return fail(MBOTS_E_INVALID, "rows too large");
+    if (device < 0) {
+        unpack_learner_host(static_cast<const uint8_t *>(records), rows, with_depth != 0, *out);
+        return MBOTS_OK;
+    }
+    if ((reinterpret_cast<uintptr_t>(records) & 15u) != 0)
+        return fail(MBOTS_E_INVALID, "records must be 16-byte aligned");
+    HIP_TRY(hipSetDevice(device));
+    HIP_TRY(mbots::launch_unpack_learner(records, (uint32_t)rows, with_depth ? 1 : 0, *out, as_stream(stream)));
+    return MBOTS_OK;
+}
+
+int mbots_num_rows(mbots_handle *h, uint32_t *out)
+{
+    if (!h || !out) return fail(MBOTS_E_INVALID, "null argument");
+    if (h->cpu) {
+        *out = h->cpu->num_rows();
+        return MBOTS_OK;
+    }
+    int rc = sync_totals(h);
+    if (rc) return rc;
+    *out = h->h_totals[mbots::kTotRows];
+    return MBOTS_OK;
+}
+
+int mbots_write_actions(mbots_handle *h, const int32_t *action, const float *hidden, uint64_t rows, void *stream)
+{
+    if (!h) return fail(MBOTS_E_INVALID, "null handle");
+    uint32_t N = 0, R = 0;
+    int rc = mbots_num_agents(h, &N);
+    if (!rc) rc = mbots_num_rows(h, &R);
+    if (rc) return rc;
+    if (rows != N && rows != R) return fail(MBOTS_E_INVALID, "rows must be num_agents() or num_rows()");
+    if (h->cpu) {
+        mbots::cpu::Table &t = h->cpu->table();
+        if (action && rows) memcpy(t.action.data(), action, rows * 6 * sizeof(int32_t));
+        if (hidden && rows) memcpy(t.hidden.data(), hidden, rows * mbots::kHidden * sizeof(float));
+        return MBOTS_OK;
+    }
+    HIP_TRY(hipSetDevice(h->device));
+    hipStream_t st = as_stream(stream);
+    if ((rc = use_stream(h, st))) return rc;
+    const int tb = h->tb;
+    const int owed = pending_mask(h);
+    // a column written only in part keeps its other rows: copied out of an
+    // aliased Prev storage first; a column written whole is simply written
+    const int part = (action && rows < R && h->a_alias[tb] ? 1 : 0) | (hidden && rows < R && h->h_alias[tb] ? 2 : 0);
+    if ((rc = materialize_cur_ah(h, st, part))) return rc;
+    note_use(h, mbots::kMoveAH, owed);
+    const mbots::ObsTable &t = h->T[tb];
+    if (action && rows) HIP_TRY(hipMemcpyAsync(t.action, action, rows * 6 * sizeof(int32_t), hipMemcpyDefault, st));
+    if (hidden && rows)
+        HIP_TRY(hipMemcpyAsync(t.hidden, hidden, rows * mbots::kHidden * sizeof(float), hipMemcpyDefault, st));
+    if (action) h->a_alias[tb] = false;
+    if (hidden) h->h_alias[tb] = false;
+    return MBOTS_OK;
 }
 
 int mbots_unpack_rollout(const void *records, uint64_t rows, int32_t with_depth, int32_t device, float *obs,
@@ -988,8 +1172,8 @@ int mbots_unpack_rollout(const void *records, uint64_t rows, int32_t with_depth,
         unpack_rollout_host(static_cast<const uint8_t *>(records), rows, with_depth != 0, obs, reward, stats);
         return MBOTS_OK;
     }
-    if (stats && (reinterpret_cast<uintptr_t>(stats) & 15u))
-        return fail(MBOTS_E_INVALID, "stats must be 16-byte aligned");
+    if ((stats && (reinterpret_cast<uintptr_t>(stats) & 15u)) || (reinterpret_cast<uintptr_t>(records) & 15u))
+        return fail(MBOTS_E_INVALID, "records and stats must be 16-byte aligned");
     HIP_TRY(hipSetDevice(device));
     HIP_TRY(mbots::launch_unpack_rollout(records, (uint32_t)rows, with_depth ? 1 : 0, obs, reward, stats,
                                          as_stream(stream)));
@@ -1001,6 +1185,8 @@ int mbots_join(mbots_handle *h, void *stream)
     if (!h) return fail(MBOTS_E_INVALID, "null handle");
     if (h->cpu) return MBOTS_OK;   // synchronous: nothing outstanding
     HIP_TRY(hipSetDevice(h->device));
+    int rc = use_stream(h, as_stream(stream));
+    if (rc) return rc;
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     unsigned long long cid = 0;
     HIP_TRY(hipStreamGetCaptureInfo(as_stream(stream), &cs, &cid));
@@ -1075,7 +1261,7 @@ int mbots_save_checkpoint(mbots_handle *h, void *dst, uint64_t bytes)
     HIP_TRY(hipSetDevice(h->device));
     int rc0 = materialize_prev(h, h->last_stream);
     if (!rc0) rc0 = materialize_prev_ah(h, h->last_stream);
-    if (!rc0) rc0 = materialize_cur_ah(h, h->last_stream);
+    if (!rc0) rc0 = materialize_cur_ah(h, h->last_stream, 3);
     if (!rc0) rc0 = materialize_psem(h, h->last_stream);
     if (rc0) return rc0;
     HIP_TRY(hipDeviceSynchronize());   // the sensor's finder / semantic rows included
@@ -1149,9 +1335,12 @@ int mbots_load_checkpoint(mbots_handle *h, const void *src, uint64_t bytes)
     h->prefetched = 0;
     h->steps = 1;
     hipStream_t st = nullptr;
+    h->last_stream = st;
     int rc = record_totals(h, st);
     if (rc) return rc;
     HIP_TRY(hipDeviceSynchronize());
+    if (h->h_totals[mbots::kTotRows] != hd.n_rows)
+        return fail(MBOTS_E_INVALID, "checkpoint row count disagrees with its saved totals");
     return MBOTS_OK;
 }
 

@@ -1,4 +1,5 @@
-"""Rollout gather to the learner rank (BASELINE config 5).
+"""Rollout gather to the learner rank and the learner's writes back
+(BASELINE config 5).
 
 Each rank steps its own world shard ([r*W, (r+1)*W), no collective on the
 step) and exports species-major rows.  The learner (PPO, learn/train.py --
@@ -14,6 +15,19 @@ consumes there:
      exactly the table one device holding every world would export.
 
     out = gather_rollout({"obs": obs, "reward": rew}, species_rows, dst=0)
+
+The full round trip the reference training loop makes after every step
+(learn/training_loop.py:36-137):
+
+    got, plan = gather_learner(mgr, dst=0)          # what :43-93 read
+    if rank == 0: actions, memory = learner(got)    # [sum N_r, 6] / [sum N_r, 16]
+    mgr.shift_observations()                        # :135
+    scatter_actions(mgr, actions, memory, plan)     # :136-137, to the owning ranks
+
+scatter_actions also sends every rank but the last the rows of its shard
+ghost (the next rank's first world, SimManager(shard_ghost=True)), so the
+ghost acts as that world does on its own rank and the faithful B.3 reward
+(sim.cpp:943) of the shard's last world equals one device's under a learner.
 """
 import torch
 import torch.distributed as dist
@@ -71,6 +85,106 @@ def gather_records(mgr, dst=0, group=None):
         return None
     recs = reassemble([b[:n_max] for b in bufs], all_cnt)
     return mb.unpack_rollout(recs.to(dev))
+
+
+def _counts_device(mgr, group):
+    return mgr.device if dist.get_backend(group) == "nccl" else torch.device("cpu")
+
+
+def exchange_plan(mgr, group=None):
+    """all_gather of every rank's per-species row counts and its first world's
+    species counts (the rows of the previous rank's shard ghost): the plan the
+    reassembly (gather) and its inverse (scatter_actions) follow."""
+    world = dist.get_world_size(group)
+    counts = mgr.species_count_tensor().to_torch()
+    cdev = _counts_device(mgr, group)
+    mine = torch.cat([counts.sum(dim=0).to(torch.int64), counts[0].to(torch.int64)]).to(cdev)
+    allc = [torch.zeros_like(mine) for _ in range(world)]
+    dist.all_gather(allc, mine, group=group)
+    allc = torch.stack(allc).cpu()
+    return {"counts": allc[:, :4], "first": allc[:, 4:]}
+
+
+def gather_learner(mgr, dst=0, group=None, keys=None):
+    """Config 5, learner side of the step: every rank packs its export rows'
+    learner records (SimManager.pack_learner: current and previous observation
+    columns, reward, stats, Action, HiddenState, PrevHiddenState -- what
+    learn/training_loop.py:43-93 reads), one padded gather ships them to `dst`,
+    which reassembles the global (species, world, slot) order and unpacks them
+    (madrona_bots.unpack_learner).  Returns (tensors on `dst` / None elsewhere,
+    plan) -- the plan is scatter_actions' argument."""
+    import madrona_bots as mb
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    dst_global = dst if group is None else dist.get_global_rank(group, dst)
+    dev = mgr.device
+    cdev = _counts_device(mgr, group)
+    plan = exchange_plan(mgr, group)
+    all_cnt = plan["counts"]
+    n_max = int(all_cnt.sum(dim=1).max())
+    rb = mgr.learner_record_bytes()
+    pad = torch.empty((max(n_max, 1), rb), dtype=torch.uint8, device=dev)   # rows past N: padding
+    mgr.pack_learner(pad)
+    send = pad if cdev.type == dev.type else pad.to(cdev)
+    bufs = [torch.empty_like(send) for _ in range(world)] if rank == dst else None
+    dist.gather(send, bufs, dst=dst_global, group=group)
+    if rank != dst:
+        return None, plan
+    recs = reassemble([b[:n_max] for b in bufs], all_cnt)
+    kw = {} if keys is None else {"keys": keys}
+    return mb.unpack_learner(recs.to(dev), **kw), plan
+
+
+def split_rows(glob, plan, r):
+    """Inverse of reassemble for rank r: its own rows (species-major) and then
+    its shard ghost's (r < ranks - 1: the next rank's first world, species by
+    species) out of the global (species, world, slot) order."""
+    cnt, first = plan["counts"], plan["first"]
+    ranks = cnt.shape[0]
+    tot = cnt.sum(dim=0)
+    parts = []
+
+    def seg(s, q, n):
+        off = int(tot[:s].sum()) + int(cnt[:q, s].sum())
+        parts.append(glob[off:off + n])
+    for s in range(4):
+        seg(s, r, int(cnt[r, s]))
+    if r < ranks - 1:
+        for s in range(4):
+            seg(s, r + 1, int(first[r + 1, s]))
+    return torch.cat(parts)
+
+
+def scatter_actions(mgr, actions, memory, plan, src=0, group=None):
+    """The learner's writes (training_loop.py:136-137) sent to the ranks that
+    own the rows: on `src`, int32 [sum N_r, 6] actions and
+    float32 [sum N_r, 16] memory in the global order gather_learner produced;
+    every rank receives its rows (plus its shard ghost's) in one padded
+    scatter and writes them with SimManager.write_actions."""
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    src_global = src if group is None else dist.get_global_rank(group, src)
+    dev = mgr.device
+    cdev = _counts_device(mgr, group)
+    cnt, first = plan["counts"], plan["first"]
+    rows = [int(cnt[r].sum()) + (int(first[r + 1].sum()) if r < world - 1 else 0) for r in range(world)]
+    r_max = max(max(rows), 1)
+    recv = torch.empty((r_max, 22), dtype=torch.int32, device=cdev)
+    chunks = None
+    if rank == src:
+        both = torch.cat([actions.to(torch.int32), memory.to(torch.float32).view(torch.int32)], dim=1).to(cdev)
+        chunks = []
+        for r in range(world):
+            part = split_rows(both, plan, r)
+            buf = torch.zeros((r_max, 22), dtype=torch.int32, device=cdev)
+            buf[:part.shape[0]] = part
+            chunks.append(buf)
+    dist.scatter(recv, chunks, src=src_global, group=group)
+    mine = recv[:rows[rank]].to(dev)
+    if mine.shape[0] != mgr.num_rows():
+        raise RuntimeError(f"rank {rank}: {mine.shape[0]} rows received, the table holds {mgr.num_rows()} "
+                           "(is shard_ghost set on every rank but the last?)")
+    mgr.write_actions(mine[:, :6].contiguous(), mine[:, 6:].contiguous().view(torch.float32))
 
 
 def gather_rollout(tensors, rows_per_species, dst=0, group=None):

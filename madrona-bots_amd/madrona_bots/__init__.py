@@ -24,7 +24,7 @@ import types
 
 import torch  # loads the HIP runtime libmbots.so links against (same soname)
 
-__all__ = ["SimManager", "Tensor", "madrona", "ExportID", "ExecMode", "unpack_rollout"]
+__all__ = ["SimManager", "Tensor", "madrona", "ExportID", "ExecMode", "unpack_rollout", "unpack_learner"]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # MBOTS_LIB: developer override to A/B alternative builds of the same library
@@ -42,6 +42,11 @@ class _Config(ctypes.Structure):
                 ("sensor_size", ctypes.c_uint32), ("world_offset", ctypes.c_uint32),
                 ("agent_capacity", ctypes.c_uint32), ("flags", ctypes.c_uint32),
                 ("exec_mode", ctypes.c_int32)]
+
+
+class _LearnerOut(ctypes.Structure):
+    _fields_ = [(k, ctypes.c_void_p) for k in
+                ("obs", "prev_obs", "reward", "stats", "action", "hidden", "prev_hidden")]
 
 
 class _CTensor(ctypes.Structure):
@@ -65,6 +70,7 @@ def _load():
         "mbots_load_checkpoint": [vp, vp, ctypes.c_uint64],
         "mbots_world_state": [vp, u32, vp, vp, vp, vp, P(i32)],
         "mbots_export": [vp, i32, P(_CTensor)],
+        "mbots_export_on": [vp, i32, vp, P(_CTensor)],
         "mbots_set_action": [vp, u32, P(i32)],
         "mbots_agent_offset_for_world": [vp, u32, P(u32)],
         "mbots_write_synthetic_actions": [vp, u32, u32, i32, vp],
@@ -72,6 +78,11 @@ def _load():
         "mbots_rollout_record_bytes": [vp, P(u32)],
         "mbots_pack_rollout": [vp, vp, ctypes.c_uint64, vp],
         "mbots_unpack_rollout": [vp, ctypes.c_uint64, i32, i32, vp, vp, vp, vp],
+        "mbots_learner_record_bytes": [vp, P(u32)],
+        "mbots_pack_learner": [vp, vp, ctypes.c_uint64, vp],
+        "mbots_unpack_learner": [vp, ctypes.c_uint64, i32, i32, P(_LearnerOut), vp],
+        "mbots_write_actions": [vp, vp, vp, ctypes.c_uint64, vp],
+        "mbots_num_rows": [vp, P(u32)],
         "mbots_agent_steps": [vp, P(ctypes.c_uint64)],
         "mbots_overflow": [vp, P(ctypes.c_uint64)],
         "mbots_enable_kernel_timing": [vp, i32],
@@ -211,6 +222,38 @@ def unpack_rollout(records, with_depth=None):
     return {"obs": obs, "reward": rew, "stats": st}
 
 
+LEARNER_BYTES, LEARNER_BYTES_DEPTH = 272, 336
+_LEARNER_KEYS = ("obs", "prev_obs", "reward", "stats", "action", "hidden", "prev_hidden")
+
+
+def unpack_learner(records, with_depth=None, keys=_LEARNER_KEYS):
+    """Learner side of the config-5 round trip: uint8 [N, 272 | 336] learner
+    records (SimManager.pack_learner, gathered from every rank) -> the columns
+    learn/training_loop.py reads after step(): "obs" / "prev_obs" float32
+    [N, 69] (construct_obs of the current / previous columns, bit-identical),
+    "reward" [N, 1], "stats" int32 [N, 4], "action" int32 [N, 6], "hidden" /
+    "prev_hidden" float32 [N, 16] (mbots_unpack_learner), on the records'
+    device; `keys` selects the outputs."""
+    if records.dtype != torch.uint8 or records.dim() != 2 or \
+            records.shape[1] not in (LEARNER_BYTES, LEARNER_BYTES_DEPTH):
+        raise ValueError(f"records must be uint8 [N, {LEARNER_BYTES}] or [N, {LEARNER_BYTES_DEPTH}]")
+    depth = records.shape[1] == LEARNER_BYTES_DEPTH if with_depth is None else bool(with_depth)
+    if depth != (records.shape[1] == LEARNER_BYTES_DEPTH):
+        raise ValueError("with_depth does not match the record width")
+    rec = records.contiguous()
+    n, dev = rec.shape[0], rec.device
+    shapes = {"obs": ((n, OBS_DIM), torch.float32), "prev_obs": ((n, OBS_DIM), torch.float32),
+              "reward": ((n, 1), torch.float32), "stats": ((n, 4), torch.int32),
+              "action": ((n, 6), torch.int32), "hidden": ((n, 16), torch.float32),
+              "prev_hidden": ((n, 16), torch.float32)}
+    out = {k: torch.empty(shapes[k][0], dtype=shapes[k][1], device=dev) for k in keys}
+    lo = _LearnerOut(**{k: (out[k].data_ptr() if k in out else None) for k in _LEARNER_KEYS})
+    stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream if dev.type == "cuda" else None)
+    _check(_lib.mbots_unpack_learner(ctypes.c_void_p(rec.data_ptr()), n, 1 if depth else 0,
+                                     dev.index if dev.type == "cuda" else -1, ctypes.byref(lo), stream))
+    return out
+
+
 madrona = types.ModuleType("madrona_bots.madrona")
 madrona.ExecMode = ExecMode
 madrona.Tensor = Tensor
@@ -271,8 +314,14 @@ class SimManager:
 
     # -- exports ------------------------------------------------------------
     def _export(self, eid):
+        # stream-ordered on torch's current stream: the view's deferred copies
+        # and joins are enqueued there, after everything the manager enqueued
+        # on whatever stream its previous call used (mbots_export_on)
         ct = _CTensor()
-        _check(_lib.mbots_export(self._h, eid, ctypes.byref(ct)))
+        if getattr(_lib, "mbots_export_on", None) is None:   # an older build under MBOTS_LIB (A/B)
+            _check(_lib.mbots_export(self._h, eid, ctypes.byref(ct)))
+        else:
+            _check(_lib.mbots_export_on(self._h, eid, self._stream(), ctypes.byref(ct)))
         return Tensor(self, ct)
 
     def depth_tensor(self, is_prev=False):
@@ -371,6 +420,61 @@ class SimManager:
         _check(_lib.mbots_pack_rollout(self._h, ctypes.c_void_p(out.data_ptr()), out.shape[0],
                                        self._stream()))
         return out[:n]
+
+    def num_rows(self):
+        """Every table row: num_agents() plus the shard ghost's rows (which
+        follow row N; see write_actions)."""
+        v = ctypes.c_uint32()
+        _check(_lib.mbots_num_rows(self._h, ctypes.byref(v)))
+        return v.value
+
+    def learner_record_bytes(self):
+        """Bytes per learner record (include/mbots.h: 272, or 336 with real depth)."""
+        v = ctypes.c_uint32()
+        _check(_lib.mbots_learner_record_bytes(self._h, ctypes.byref(v)))
+        return v.value
+
+    def pack_learner(self, out=None):
+        """Everything the reference training loop reads after step() --
+        current and previous observation columns, reward, stats, Action,
+        HiddenState, PrevHiddenState (learn/training_loop.py:43-93) -- as one
+        uint8 [N, learner_record_bytes()] record per export row: the payload of
+        the config-5 gather (harness/gather.py); unpack_learner() rebuilds the
+        learner's tensors.  `out` may hold more rows (padding)."""
+        n = self.num_agents()
+        rb = self.learner_record_bytes()
+        if out is None:
+            out = torch.empty((n, rb), dtype=torch.uint8, device=self.device)
+        if out.dtype != torch.uint8 or out.device != self.device or not out.is_contiguous() \
+                or out.dim() != 2 or out.shape[1] != rb or out.shape[0] < n:
+            raise ValueError(f"out must be a contiguous uint8 [>= {n}, {rb}] tensor on {self.device}")
+        _check(_lib.mbots_pack_learner(self._h, ctypes.c_void_p(out.data_ptr()), out.shape[0],
+                                       self._stream()))
+        return out[:n]
+
+    def write_actions(self, actions=None, memory=None):
+        """The learner's writes for every row at once (training_loop.py:136-137:
+        action_tensor[...] = one_hot; memory_tensor[...] = new_memory):
+        int32 [R, 6] actions and/or float32 [R, 16] memory, R = num_agents() or
+        num_rows() (the latter also drives the shard ghost's agents, which then
+        act exactly as the next rank's first world does) -- mbots_write_actions."""
+        def arg(t, cols, dtype):
+            if t is None:
+                return None, None
+            if t.dtype != dtype or t.dim() != 2 or t.shape[1] != cols or t.device != self.device:
+                raise ValueError(f"expected {dtype} [rows, {cols}] on {self.device}")
+            t = t.contiguous()
+            return t, t.shape[0]
+        a, ra = arg(actions, 6, torch.int32)
+        m, rm = arg(memory, 16, torch.float32)
+        rows = ra if ra is not None else rm
+        if rows is None:
+            return
+        if ra is not None and rm is not None and ra != rm:
+            raise ValueError("actions and memory must have the same rows")
+        _check(_lib.mbots_write_actions(self._h, ctypes.c_void_p(a.data_ptr() if a is not None else None),
+                                        ctypes.c_void_p(m.data_ptr() if m is not None else None), rows,
+                                        self._stream()))
 
     def save_checkpoint(self, path=None):
         """Live simulator state as bytes (and to `path` if given); see

@@ -16,6 +16,11 @@
    shift_observations(), and the full final tables.  The HIP path is checked
    against these in tests/test_parity_gpu.py, the oracle itself in
    tests/test_golden.py.
+3. oracle_w4096_a32_s69_h120.npz -- the bench's horizon:
+   BASELINE config 2's 4096 worlds driven for 120 steps by bench.py's loop
+   (identity-keyed one-hot actions, seed 1234, no memory writes; step, shift),
+   per-step digests only (the tables themselves would be ~35 MB).  Checked
+   against the HIP path in tests/test_parity_horizon.py.
 
     python tests/golden/make_golden.py
 """
@@ -78,6 +83,24 @@ def save_fixture(name, W, A, seed, steps, reward_fixed, cap):
     meta = {"worlds": W, "agents": A, "seed": seed, "steps": steps, "reward_fixed": reward_fixed,
             "cap": cap, "action_seed": 1234, "write_hidden": True, "log": log}
     np.savez_compressed(os.path.join(HERE, name + ".npz"), meta=json.dumps(meta), **arrays)
+    print(f"{name}: {sim.num_agents()} agents after {steps} steps")
+
+
+HORIZON = ("oracle_w4096_a32_s69_h120", 4096, 32, 69, 120)
+
+
+def save_horizon(name, W, A, seed, steps, threads=8):
+    sim = pyoracle.OracleSim(W, seed, A, num_threads=threads)
+    log = [("init", sim.num_agents(), table_digests(sim))]
+    for t in range(steps):
+        sim.write_synthetic_actions(1234, t, False)   # bench.py: write_synthetic_actions(ACTION_SEED, t)
+        sim.step()
+        log.append((f"step{t}", sim.num_agents(), table_digests(sim)))
+        sim.shift_observations()
+        log.append((f"shift{t}", sim.num_agents(), table_digests(sim)))
+    meta = {"worlds": W, "agents": A, "seed": seed, "steps": steps, "reward_fixed": False, "cap": 128,
+            "action_seed": 1234, "write_hidden": False, "overflow": int(sim.overflow()), "log": log}
+    np.savez_compressed(os.path.join(HERE, name + ".npz"), meta=json.dumps(meta))
     print(f"{name}: {sim.num_agents()} agents after {steps} steps")
 
 
@@ -150,6 +173,7 @@ def main():
         print("reference_shapes.json written")
     for fx in FIXTURES:
         save_fixture(*fx)
+    save_horizon(*HORIZON)
 
 
 if __name__ == "__main__":

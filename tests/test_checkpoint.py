@@ -148,3 +148,27 @@ def test_set_action_after_step_then_shift():
     assert prev[3].tolist() == [1, 0, 1, 0, 1, 0]
     assert torch.equal(prev, cur)
     assert before.shape[1] == 6
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ghost", [False, True])
+def test_checkpoint_load_then_save_before_stepping(ghost):
+    """a restored manager saved again before any step writes the
+    same blob (the table's row count -- every row, the shard ghost's included,
+    kCkptVersion 3 -- comes back with the state), and an older version's blob
+    is refused."""
+    import madrona_bots as mb
+    kw = dict(shard_ghost=ghost)
+    a = mb.SimManager(0, 64, 5, 32, **kw)
+    _run(a, 0, 7)
+    blob = a.save_checkpoint()
+    b = mb.SimManager(0, 64, 5, 32, **kw)
+    b.load_checkpoint(blob)
+    assert b.num_rows() == a.num_rows() > b.num_agents() if ghost else b.num_rows() == a.num_rows()
+    again = b.save_checkpoint()
+    assert np.array_equal(blob, again)
+    old = blob.copy()
+    old[8:12] = np.frombuffer(np.uint32(2).tobytes(), np.uint8)   # header version field
+    c = mb.SimManager(0, 64, 5, 32, **kw)
+    with pytest.raises(RuntimeError, match="version"):
+        c.load_checkpoint(old)

@@ -1,0 +1,223 @@
+"""The config-5 learner round trip (BASELINE config 5; SURVEY 8e steps 1-3;
+learn/training_loop.py:36-137): after every step the learner's reads travel to
+rank 0 as learner records (harness/gather.py gather_learner: current and
+previous observation columns, reward, stats, Action, HiddenState,
+PrevHiddenState), rank 0 chooses actions and memory from them, and
+scatter_actions writes them back into the rows of the ranks that own them --
+the shard ghosts' rows included, so the faithful B.3 reward (sim.cpp:943) of a
+shard's last world stays one device's.
+
+Checked bitwise every step against one manager holding every world that
+receives the same actions through write_actions (the whole-table form of
+training_loop.py:136-137's view writes): the gathered tensors == that
+manager's own views (construct_obs, reward, stats, action, hidden state and
+their previous forms), and therefore its next steps.
+"""
+import os
+import sys
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HARNESS = os.path.join(ROOT, "madrona-bots_amd", "harness")
+SEED = 69
+
+
+def _learner(got, t):
+    """A deterministic stand-in for the PPO step (learn/models.py, out of
+    scope): one-hot actions and new memory computed from what was gathered."""
+    bits = got["obs"].view(torch.int32).to(torch.int64).sum(dim=1) + got["action"].to(torch.int64).sum(dim=1) * 7
+    k = (bits + t) % 6
+    actions = torch.nn.functional.one_hot(k, 6).to(torch.int32)
+    memory = got["obs"][:, :16] * 0.25 + got["hidden"] * 0.5 - got["prev_hidden"] * 0.125
+    return actions, memory
+
+
+def _own_views(m):
+    """What training_loop.py reads, straight from one manager's views."""
+    return {"obs": m.construct_obs(False), "prev_obs": m.construct_obs(True),
+            "reward": m.reward_tensor(False).to_torch().clone(),
+            "stats": m.stats_tensor(False).to_torch().clone(),
+            "action": m.action_tensor(False).to_torch().clone(),
+            "hidden": m.hidden_state_tensor(False).to_torch().clone(),
+            "prev_hidden": m.hidden_state_tensor(True).to_torch().clone()}
+
+
+def _bitwise(a, b):
+    return a.shape == b.shape and torch.equal(a.contiguous().view(torch.int32).cpu(),
+                                              b.contiguous().view(torch.int32).cpu())
+
+
+def _roundtrip_in_process(shards, full, steps):
+    """Shards and the full manager in one process: the gather / scatter data
+    movement of harness/gather.py without the collectives (the reassembly and
+    its inverse are the same functions)."""
+    sys.path.insert(0, HARNESS)
+    import gather
+    import madrona_bots as mb
+    bad = []
+    for m in shards + [full]:
+        m.write_synthetic_actions(1234, 0, True)
+    for t in range(steps):
+        for m in shards + [full]:
+            m.step()
+        counts = [m.species_count_tensor().to_torch() for m in shards]
+        plan = {"counts": torch.stack([c.sum(dim=0).to(torch.int64).cpu() for c in counts]),
+                "first": torch.stack([c[0].to(torch.int64).cpu() for c in counts])}
+        recs = gather.reassemble([m.pack_learner() for m in shards], plan["counts"])
+        got = mb.unpack_learner(recs)
+        ref = _own_views(full)
+        bad += [f"step {t}: {k}" for k in ref if not _bitwise(got[k], ref[k])]
+        actions, memory = _learner(got, t)
+        for m in shards + [full]:
+            m.shift_observations()
+        full.write_actions(actions, memory)
+        both = torch.cat([actions, memory.view(torch.int32)], dim=1)
+        for r, m in enumerate(shards):
+            part = gather.split_rows(both, plan, r)
+            assert part.shape[0] == m.num_rows()
+            m.write_actions(part[:, :6].contiguous(), part[:, 6:].contiguous().view(torch.float32))
+    return bad
+
+
+@pytest.mark.parametrize("fix_depth", [False, True])
+def test_learner_roundtrip_cpu_shards_equal_one(fix_depth):
+    """CPU mode: 2 shards x 6 worlds (faithful rewards through the ghost) ==
+    one 12-world manager under learner-chosen actions and memory."""
+    import madrona_bots as mb
+    W = 6
+    kw = dict(exec_mode="cpu", fix_depth_alias=fix_depth)
+    shards = [mb.SimManager(0, W, SEED, 32, world_offset=r * W, shard_ghost=r == 0, **kw) for r in range(2)]
+    full = mb.SimManager(0, 2 * W, SEED, 32, **kw)
+    assert _roundtrip_in_process(shards, full, 6) == []
+
+
+def test_split_rows_inverts_reassemble():
+    sys.path.insert(0, HARNESS)
+    import gather
+    cnt = torch.tensor([[3, 1, 0, 2], [2, 2, 1, 0], [1, 0, 4, 1]])
+    first = torch.tensor([[1, 0, 0, 1], [1, 1, 0, 0], [0, 0, 2, 1]])
+    n = int(cnt.sum())
+    glob = torch.arange(n)
+    plan = {"counts": cnt, "first": first}
+    own = [gather.split_rows(glob, plan, r)[:int(cnt[r].sum())] for r in range(3)]
+    assert torch.equal(gather.reassemble(own, cnt), glob)
+    # rank 0's ghost rows are rank 1's first world: the first rows of each of
+    # rank 1's species segments
+    ghost = gather.split_rows(glob, plan, 0)[int(cnt[0].sum()):]
+    tot = cnt.sum(dim=0)
+    exp = [int(tot[:s].sum()) + int(cnt[0, s]) + k for s in range(4) for k in range(int(first[1, s]))]
+    assert ghost.tolist() == exp
+    assert gather.split_rows(glob, plan, 2).shape[0] == int(cnt[2].sum())
+
+
+def _worker(rank, world, port, q, steps):
+    sys.path[:0] = [HARNESS, os.path.join(ROOT, "madrona-bots_amd")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import gather
+        import madrona_bots as mb
+        W = 5
+        sim = mb.SimManager(0, W, SEED, 32, world_offset=rank * W, shard_ghost=rank < world - 1, exec_mode="cpu")
+        full = mb.SimManager(0, world * W, SEED, 32, exec_mode="cpu") if rank == 0 else None
+        for m in (sim, full):
+            if m is not None:
+                m.write_synthetic_actions(1234, 0, True)
+        bad = []
+        for t in range(steps):
+            sim.step()
+            got, plan = gather.gather_learner(sim, dst=0)
+            actions = memory = None
+            if rank == 0:
+                full.step()
+                ref = _own_views(full)
+                bad += [f"step {t}: {k}" for k in ref if not _bitwise(got[k], ref[k])]
+                actions, memory = _learner(got, t)
+                full.shift_observations()
+                full.write_actions(actions, memory)
+            sim.shift_observations()
+            gather.scatter_actions(sim, actions, memory, plan, src=0)
+        if rank == 0:
+            q.put(bad)
+    finally:
+        dist.destroy_process_group()
+
+
+def _spawn(target, world, *args):
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=target, args=(r, world, port, q) + args) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=240)
+        assert p.exitcode == 0
+    return q.get(timeout=5)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_learner_roundtrip_gloo(world):
+    """gather_learner / scatter_actions over gloo with 2 and 3 CPU-mode ranks:
+    rank 0's gathered tensors equal one manager of every world, step after
+    step, while the learner's actions drive both."""
+    assert _spawn(_worker, world, 5) == []
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fix_depth", [False, True])
+def test_learner_roundtrip_hip_shards_equal_one(fix_depth):
+    """HIP: 2 shards x 1024 worlds on the device (faithful rewards through the
+    ghost) == one 2048-world manager under learner-chosen actions and memory,
+    every gathered tensor bitwise, 8 steps."""
+    import madrona_bots as mb
+    W = 1024
+    kw = dict(fix_depth_alias=fix_depth)
+    shards = [mb.SimManager(0, W, SEED, 32, world_offset=r * W, shard_ghost=r == 0, **kw) for r in range(2)]
+    full = mb.SimManager(0, 2 * W, SEED, 32, **kw)
+    assert _roundtrip_in_process(shards, full, 8) == []
+
+
+def _rccl_worker(rank, world, port, q):
+    sys.path[:0] = [HARNESS, os.path.join(ROOT, "madrona-bots_amd")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        import gather
+        import madrona_bots as mb
+        sim = mb.SimManager(0, 512, SEED, 32)
+        ref_m = mb.SimManager(0, 512, SEED, 32)
+        for m in (sim, ref_m):
+            m.write_synthetic_actions(1234, 0, True)
+        bad = []
+        for t in range(4):
+            sim.step()
+            ref_m.step()
+            got, plan = gather.gather_learner(sim, dst=0)
+            ref = _own_views(ref_m)
+            bad += [f"step {t}: {k}" for k in ref if not _bitwise(got[k], ref[k])]
+            actions, memory = _learner(got, t)
+            sim.shift_observations()
+            ref_m.shift_observations()
+            gather.scatter_actions(sim, actions, memory, plan, src=0)
+            ref_m.write_actions(actions, memory)
+        torch.cuda.synchronize()
+        q.put(bad)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_learner_roundtrip_over_rccl_one_rank():
+    """The round trip's collectives (all_gather of the plan, gather of the
+    learner records, scatter of actions + memory) executed by RCCL on the
+    device at one rank: equal to a manager driven through write_actions."""
+    assert _spawn(_rccl_worker, 1) == []
