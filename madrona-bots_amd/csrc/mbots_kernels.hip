@@ -13,6 +13,13 @@
 // (current observations, reward, old->new row map) -> K4 move (Action, Hidden,
 // Prev*, prev sensor to the new rows).  shift_observations() = K5 shift.
 // DESIGN.md section 4 has the schedule and each kernel's bound.
+// Probe switches (MB_COUNT, MB_SKIP_*, MB_PROBE_ALL_DEEP) build instruction-
+// count and timing probes whose rows are wrong.  They need MB_PROBE_BUILD,
+// which only scripts/build_var.sh probe builds pass (the Makefile refuses it).
+#if (defined(MB_COUNT) || defined(MB_SKIP_WIDE) || defined(MB_SKIP_P2) || defined(MB_SKIP_OUT) || \
+     defined(MB_PROBE_ALL_DEEP)) && !defined(MB_PROBE_BUILD)
+#error "probe switches give wrong rows: build probes into build_var/ with -DMB_PROBE_BUILD, never the product"
+#endif
 #include <hip/hip_ext.h>
 #include "mbots_kernels.hpp"
 #include <stdlib.h>

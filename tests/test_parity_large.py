@@ -58,9 +58,10 @@ def test_parity_8192_worlds_one_wave_sensor():
     _pair(8192, steps=4)
 
 
-@pytest.mark.timeout(600)
+@pytest.mark.timeout(900)
 def test_parity_config3_65536_worlds():
-    mgr, orc = _pair(65536, steps=5)
+    # 20 steps: every column after every step and shift
+    mgr, orc = _pair(65536, steps=20)
     assert mgr.overflow() == orc.overflow() == 0
 
 
