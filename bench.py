@@ -267,6 +267,51 @@ def reference_loop(W, args, rank, world_size, dev, distributed, label):
             "kernel_ms": ktimes}
 
 
+def bare_loop(W, args, rank, world_size, dev, distributed, label):
+    """The headline's loop -- step(), shift_observations(), the next one-hot
+    actions -- on a shard of W worlds per rank (BASELINE config 2 at W = 4096:
+    the metric's other half measured on the headline's workload); wall clock of
+    the timed steps, max over ranks; its own HBM roofline (B_step / step time)."""
+    import madrona_bots as mb
+    m = mb.SimManager(dev.index, W, SEED, AGENTS_PER_WORLD, world_offset=rank * W,
+                      shard_ghost=rank < world_size - 1)
+    # short steps: time at least 400 so a host hiccup does not move the line
+    steps = max(args.steps, 400)
+    m.write_synthetic_actions(ACTION_SEED, 0)
+    for t in range(args.warmup):
+        m.step(); m.shift_observations(); m.write_synthetic_actions(ACTION_SEED, t + 1)
+    torch.cuda.synchronize()
+    s0 = m.agent_steps()
+    if distributed:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for t in range(args.warmup, args.warmup + steps):
+        m.step(); m.shift_observations(); m.write_synthetic_actions(ACTION_SEED, t + 1)
+    torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    n_local = m.agent_steps() - s0
+    st = torch.tensor([el, float(n_local)], dtype=torch.float64, device=dev if args.backend == "nccl" else "cpu")
+    if distributed:
+        dist.barrier()
+        tm = st[0:1].clone(); dist.all_reduce(tm, op=dist.ReduceOp.MAX)
+        tot = st[1:2].clone(); dist.all_reduce(tot, op=dist.ReduceOp.SUM)
+        el, total = float(tm.item()), float(tot.item())
+    else:
+        total = float(st[1].item())
+    del m
+    n_mean = n_local / steps
+    ms = el / steps * 1e3
+    nb = algorithmic_bytes(n_mean, W)
+    gbs = nb / (ms * 1e-3) / 1e9
+    return {"worlds_per_gpu": W, "value": total / el, "unit": "agent-steps/s", "ms_per_step": ms,
+            "steps": steps, "n_gpus": world_size, "what": label, "mean_agents_per_world": n_mean / W,
+            "roofline": {"bound": "hbm", "achieved": gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": gbs / HBM_PEAK_GBS, "algorithmic_bytes_per_step": nb,
+                         "bytes": "552 N + 1952 W (SURVEY 8d)",
+                         "timing": "wall clock of the timed steps (step + shift + action write)"}}
+
+
 def spawn_ranks(args):
     """One rank per GPU for `--gpus N` when no launcher set WORLD_SIZE: this
     GPU-free parent runs torch.distributed.run as a child process (never an
@@ -495,8 +540,11 @@ def main():
             cfg5 = config5_loop(mgr, args, rank, world_size, dev, distributed)
         except Exception as e:   # reported in the line; the main measurement stands
             cfg5 = {"error": f"{type(e).__name__}: {e}"[:400]}
-    secondary = ref_main = None
+    secondary = ref_main = config2 = None
     if not args.no_secondary:
+        config2 = bare_loop(4096, args, rank, world_size, dev, distributed,
+                            "BASELINE config 2 on the headline's workload: step + shift + action write at "
+                            "4096 worlds/GPU")
         secondary = reference_loop(4096, args, rank, world_size, dev, distributed,
                                    "BASELINE config 2: random-action rollout, obs/reward tensors "
                                    "on device (learn/training_loop.py call sequence)")
@@ -615,6 +663,8 @@ def main():
                     out["sensor_valu"]["microbench_source"] = mp[0]
         if cfg5:
             out["config5"] = cfg5
+        if config2:
+            out["config2"] = config2
         if secondary:
             out["secondary"] = secondary
             out["reference_loop"] = ref_main

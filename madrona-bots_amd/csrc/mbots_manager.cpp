@@ -100,6 +100,7 @@ struct mbots_handle {
     bool prev_lazy[2] = {false, false};   // table half's six shift-owned Prev* columns are
                                           // still its current ones (lazy shift, K5)
     hipEvent_t ev_hop = nullptr;      // orders a call's stream after the last one used
+    bool totals_ok = false;           // h_totals holds the last step's counts (synchronised)
     int forced = 0;                   // deferred parts the caller's reads needed since the
                                       // last step (kMove*): the next step prefetches them
     int prefetched = 0;               // parts this step prefetched and no shift superseded
@@ -380,6 +381,11 @@ bool capturing_now(const mbots_handle *h)
 
 int sync_totals(mbots_handle *h)
 {
+    // the step's row counts are final once synchronised: later accessors of the
+    // same step skip the runtime calls (the reference loop reads ~10 views per
+    // step and is host-bound at small world counts, scripts/refhost.py) -- not
+    // once graphs exist, whose replays change the counts behind the host's back
+    if (h->totals_ok && h->cap_seen == 0) return MBOTS_OK;
     HIP_TRY(hipSetDevice(h->device));
     // a host-side row count during stream capture would be the capture-time
     // count baked into every replay (and the event wait is not capturable)
@@ -389,6 +395,7 @@ int sync_totals(mbots_handle *h)
                     "captured into a graph: capture only step / shift_observations / "
                     "write_synthetic_actions / join (device-side writers), read accessors after replay");
     HIP_TRY(hipEventSynchronize(h->ev_totals));
+    h->totals_ok = true;
     return MBOTS_OK;
 }
 
@@ -704,6 +711,7 @@ int mbots_step(mbots_handle *h, void *stream)
                                      "capture an even number (and end it with join())");
     }
     if ((rc = use_stream(h, st))) return rc;
+    h->totals_ok = false;
     const mbots::ObsTable &nxt = h->T[h->tb ^ 1];
     const int par = h->parity;
     const int lazy = h->prev_lazy[h->tb] ? 1 : 0;
@@ -1336,6 +1344,7 @@ int mbots_load_checkpoint(mbots_handle *h, const void *src, uint64_t bytes)
     h->steps = 1;
     hipStream_t st = nullptr;
     h->last_stream = st;
+    h->totals_ok = false;
     int rc = record_totals(h, st);
     if (rc) return rc;
     HIP_TRY(hipDeviceSynchronize());

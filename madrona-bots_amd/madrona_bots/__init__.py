@@ -121,6 +121,12 @@ class ExportID:
 
 _DTYPES = {0: (torch.uint8, "|u1"), 1: (torch.int8, "|i1"), 2: (torch.int32, "<i4"),
            3: (torch.float32, "<f4")}
+_DTYPE_CODE = {v[0]: k for k, v in _DTYPES.items()}
+
+
+def _raw_stream(device):
+    """hipStream_t of torch's current stream on `device` (no Stream object)."""
+    return torch._C._cuda_getCurrentRawStream(device)
 
 FLAG_REWARD_FIXED = 0x1
 FLAG_FIX_DEPTH_ALIAS = 0x2
@@ -153,8 +159,9 @@ KERNELS = ("world_step", "scan", "export", "sensor", "shift", "actions", "move",
 class Tensor:
     """Non-owning device tensor view (madrona::py::Tensor)."""
 
-    def __init__(self, owner, ct):
+    def __init__(self, owner, ct, column=False):
         self._owner = owner          # keeps the manager (and its memory) alive
+        self._column = column        # a table column: W x cap row slots behind it
         self._ptr = int(ct.data or 0)
         self._torch_dtype, self._typestr = _DTYPES[ct.dtype]
         self._device = int(ct.device)
@@ -179,6 +186,13 @@ class Tensor:
         dev = torch.device("cuda", self._device)
         if self.shape[0] == 0:
             return torch.empty(self.shape, dtype=self._torch_dtype, device=dev)
+        # one torch view per column allocation, sliced to the current row count:
+        # the learner reads ~10 views per step and is host-bound at small world
+        # counts (scripts/refhost.py); building a view from the array interface
+        # every time is most of an accessor's host cost
+        base = self._owner._view_cache(self) if self._column else None
+        if base is not None:
+            return base[:self.shape[0]]
         t = torch.as_tensor(self, device=dev)
         if t.data_ptr() != self._ptr:
             raise RuntimeError("madrona_bots: to_torch() produced a copy, expected a view")
@@ -286,6 +300,9 @@ class SimManager:
         h = ctypes.c_void_p()
         _check(_lib.mbots_create(ctypes.byref(cfg), ctypes.byref(h)))
         self._h = h
+        # row slots of every table column (the shard ghost is one more world)
+        self._cap_rows = (self.num_worlds + (1 if shard_ghost else 0)) * self.agent_capacity
+        self._views = {}
 
     def __del__(self):
         h = getattr(self, "_h", None)
@@ -296,7 +313,26 @@ class SimManager:
     def _stream(self):
         if self.exec_mode == ExecMode.CPU:
             return ctypes.c_void_p(None)
-        return ctypes.c_void_p(torch.cuda.current_stream(self.gpu_id).cuda_stream)
+        return ctypes.c_void_p(_raw_stream(self.gpu_id))
+
+    def _view_cache(self, tensor):
+        """Torch view of the whole allocation behind `tensor` (every row slot
+        the manager reserved for that column), created once; None for exports
+        that are not table columns."""
+        rows, cols = tensor.shape
+        cap_rows = self._cap_rows
+        if rows > cap_rows:
+            return None
+        key = (tensor._ptr, tensor._torch_dtype, cols)
+        base = self._views.get(key)
+        if base is None:
+            full = Tensor(None, _CTensor(tensor._ptr, _DTYPE_CODE[tensor._torch_dtype], tensor._device,
+                                         (ctypes.c_int64 * 2)(cap_rows, cols)))
+            base = torch.as_tensor(full, device=torch.device("cuda", tensor._device))
+            if base.data_ptr() != tensor._ptr:
+                raise RuntimeError("madrona_bots: to_torch() produced a copy, expected a view")
+            self._views[key] = base
+        return base
 
     @property
     def device(self):
@@ -322,7 +358,7 @@ class SimManager:
             _check(_lib.mbots_export(self._h, eid, ctypes.byref(ct)))
         else:
             _check(_lib.mbots_export_on(self._h, eid, self._stream(), ctypes.byref(ct)))
-        return Tensor(self, ct)
+        return Tensor(self, ct, column=eid not in (ExportID.SpeciesCount, ExportID.Reset))
 
     def depth_tensor(self, is_prev=False):
         return self._export(ExportID.PrevSensorDepth if is_prev else ExportID.SensorDepth)
