@@ -1047,7 +1047,33 @@ __device__ __forceinline__ void run_wide(LDS &L, const RayTab &R, int na, int a0
     const int k = lane & 31;
     const float uk = R.u[k];
     const NearPt np{R.c[k], R.s[k], R.e[k]}, fnp{R.c[kSensor], R.s[kSensor], R.e[kSensor]};
-    for (int e0 = 0; e0 < cnt; e0 += 2) {
+    // a pair left alone (the common case: most batches hold one near pair) takes
+    // 33 lanes, ray 32 being the finder (u = 0 and the finder's near point in
+    // the ray table: the same predicate), so its round evaluates one test per
+    // lane instead of a pixel's and the finder's
+    const int cnt2 = cnt & ~1;
+    if (cnt2 < cnt) {
+        const int ks = (int)lane;
+        if (ks <= kSensor) {
+            const uint32_t code = L.qcode[q0 + cnt2];
+            const int ic = (int)(code & 0x1Fu), j = (int)(code >> 11);
+            float f, l;
+            uint32_t order;
+            pair_fl(L, na, a0 + ic, j, f, l, order);
+            const float us = R.u[ks];
+            const NearPt nps{R.c[ks], R.s[ks], R.e[ks]};
+            const bool fw = (ks < 24) | (ks == kSensor);
+            uint32_t kv;
+            if (j < na) {
+                const FoodBox b = box_setup(f, l, L.frot[j], L.hd[a0 + ic]);
+                kv = box_hit(b, us, fw, nps.c) ? zkey(box_z(b, fw), order) : kNoKey;
+            } else {
+                kv = pixel_key(f, l, us, nps, fw, order);
+            }
+            if (kv != kNoKey) atomicMin(&L.key[ic * kKeyStride + ks], kv);
+        }
+    }
+    for (int e0 = 0; e0 < cnt2; e0 += 2) {
         const int e = e0 + (lane >> 5);
         if (e < cnt) {
             const uint32_t code = L.qcode[q0 + e];

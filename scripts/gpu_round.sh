@@ -6,7 +6,7 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-TAG=${TAG:-r03}
+TAG=${TAG:-r04}
 mkdir -p gpurun_out
 if [ "${TESTS:-1}" = "1" ]; then
   timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 600 --timeout-method thread \
