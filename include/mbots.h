@@ -236,7 +236,9 @@ int mbots_world_state(mbots_handle *h, uint32_t world, float *xy_rwrz, int32_t *
 
 /* Stream ordering: every call that takes a stream enqueues on it after all
  * work this manager enqueued on the stream of its previous call (an event
- * hop when the two differ; not across a graph capture's boundary). */
+ * hop when the two differ; not across a graph capture's boundary).  That
+ * previous stream must still exist when a call on another stream is made
+ * (torch's pooled streams always do). */
 /* Build utilities (benchmark / test harness, not reference API):
  * identity-keyed synthetic action stream: one-hot(threefry(seed,step |
  * global_world, slot) % 6) written into the Action column of every live agent;
