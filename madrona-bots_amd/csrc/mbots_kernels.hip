@@ -36,7 +36,8 @@ constexpr int kTileWorlds = 1024;             // worlds per scan tile (K2 block)
 #endif
 #ifndef MB_NT
 #define MB_NT 35  // non-temporal stores: 1 K4, 2 K5, 4 K3a, 8 sensor output;
-                  // non-temporal loads: 32 K4 sources, 64 K5 sources
+                  // non-temporal loads: 32 K4 sources, 64 K5 sources;
+                  // 128: K1 compaction stores
 #endif
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -546,16 +547,17 @@ __device__ void world_step(SimState &S, const ObsTable &cur, WorldLDS<kCap> &L, 
         const uint64_t m = ballot64(alive);
         if (alive) {
             const size_t d = base + nn + rank_below(m);
-            S.x_out[d] = L.x[i];
-            S.y_out[d] = L.y[i];
-            S.rw_out[d] = L.rw[i];
-            S.rz_out[d] = L.rz[i];
-            S.species_out[d] = L.species[i];
-            S.health[d] = L.accum[i];
-            S.obsrow_out[d] = i < n0 ? rows[g] : -1;   // newborns: no row
-            S.sur0[d] = L.sur0[i];
-            S.sur1[d] = L.sur1[i];
-            S.stats[d] = L.flags[i] & F_STATS;
+            constexpr bool nt = (MB_NT & 128) != 0;
+            st_stream(S.x_out + d, L.x[i], nt);
+            st_stream(S.y_out + d, L.y[i], nt);
+            st_stream(S.rw_out + d, L.rw[i], nt);
+            st_stream(S.rz_out + d, L.rz[i], nt);
+            st_stream(S.species_out + d, (int32_t)L.species[i], nt);
+            st_stream(S.health + d, L.accum[i], nt);
+            st_stream(S.obsrow_out + d, i < n0 ? rows[g] : -1, nt);   // newborns: no row
+            st_stream(S.sur0 + d, L.sur0[i], nt);
+            st_stream(S.sur1 + d, L.sur1[i], nt);
+            st_stream(S.stats + d, (uint32_t)(L.flags[i] & F_STATS), nt);
             atomicAdd(&L.scount[L.species[i] - 1], 1);
         }
         nn += __popcll(m);
@@ -701,6 +703,20 @@ __global__ __launch_bounds__(1024) void scan_kernel(SimState S, int parity)
             // make the mirror visible before the dispatch's completion signal,
             // whatever scope the runtime gives that signal's release
             __threadfence_system();
+        }
+    }
+    if (S.epoch) {
+        // the fork as a value wait ("Small world counts"): every
+        // block writes its outputs back (agent-scope release) before it counts
+        // itself done, and the last one stores the step's epoch into the
+        // signal word the sensor's queue waits on (its dispatch acquires)
+        __syncthreads();
+        if (t == 0) {
+            __threadfence();
+            if (atomicAdd(S.fork_ctr, 1u) == gridDim.x - 1u) {
+                atomicExch(S.fork_ctr, 0u);
+                __hip_atomic_store(S.sig_fork, S.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
         }
     }
 }

@@ -48,6 +48,11 @@ struct SimState {
     int32_t *obsrow_out;            // K1 -> K3a / the sensor: each slot's old export row (not
                                     // swapped: K1 reads obsrow, K3a rewrites it)
     uint64_t *food_out;
+    // the fork as a value wait (small world counts, mbots_step): K2's last
+    // block stores `epoch` into sig_fork (signal memory); epoch 0: no flag
+    uint32_t *fork_ctr;             // K2 blocks done (reset by the last)
+    uint32_t *sig_fork;
+    uint32_t epoch;
     uint32_t W, cap, A, world_offset, flags, seed, ntiles;
     uint32_t Wx;                    // exported worlds: W, or W - 1 with the shard ghost (the
                                     // last world, its rows placed after every exported row)

@@ -100,6 +100,8 @@ struct mbots_handle {
     bool prev_lazy[2] = {false, false};   // table half's six shift-owned Prev* columns are
                                           // still its current ones (lazy shift, K5)
     hipEvent_t ev_hop = nullptr;      // orders a call's stream after the last one used
+    uint32_t *sig_fork = nullptr;     // the fork's signal word (small world counts)
+    uint32_t epoch = 0;               // the last epoch K2 raised (never 0)
     bool totals_ok = false;           // h_totals holds the last step's counts (synchronised)
     int forced = 0;                   // deferred parts the caller's reads needed since the
                                       // last step (kMove*): the next step prefetches them
@@ -114,6 +116,19 @@ struct mbots_handle {
 };
 
 namespace {
+
+// The fork (K2 -> the sensor's queue) as a hipStreamWaitValue32 on a flag K2's
+// last block stores, instead of a wait on K2's completion signal: the hop is
+// ~3 us instead of ~7 (scripts/ubench/hop_latency.hip).  At small world
+// counts the step is a latency chain and that is -1 to -4 % at 4096 worlds;
+// from 16384 on the chip is throughput-bound from K1's end on and the flag's
+// fences cost about what the hop saves (±0 at 16384, +0.2-0.6 % at 65536), so
+// events there (profiles/r04_value_fork_small_ab.jsonl,
+// profiles/r04_value_waits_ab.jsonl, DESIGN_EXPERIMENTS.md round 4).
+#ifndef MB_VALUE_FORK_MAX
+#define MB_VALUE_FORK_MAX 8192
+#endif
+bool fork_by_value(uint32_t W) { return W <= MB_VALUE_FORK_MAX; }
 
 hipEvent_t get_event(mbots_handle *h)
 {
@@ -197,6 +212,7 @@ size_t layout(mbots_handle *h, Arena &a)
     S.world_off = a.take<int32_t>(W);
     S.src_of = a.take<int32_t>(rows);
     S.overflow = a.take<uint32_t>(W);
+    S.fork_ctr = a.take<uint32_t>(1);
     S.totals = a.take<uint32_t>(8);
     S.ntiles = scan_tiles((uint32_t)W);
     S.tiles = a.take<int32_t>((size_t)2 * S.ntiles * kTileBuckets * 5);
@@ -629,6 +645,12 @@ int mbots_create(const mbots_config *cfg_in, mbots_handle **out)
     constexpr unsigned kSyncEvent = hipEventDisableTiming | hipEventReleaseToDevice;
     check(hipEventCreateWithFlags(&h->ev_totals, kSyncEvent), "hipEventCreateWithFlags");
     check(hipEventCreateWithFlags(&h->ev_hop, kSyncEvent), "hipEventCreateWithFlags");
+    if (fork_by_value((uint32_t)S.W)) {
+        // the word hipStreamWaitValue32 polls (read by the command processor)
+        check(hipExtMallocWithFlags((void **)&h->sig_fork, 8, hipMallocSignalMemory), "hipExtMallocWithFlags");
+        if (rc == MBOTS_OK) check(hipMemset(h->sig_fork, 0, 8), "hipMemset");
+        S.sig_fork = h->sig_fork;
+    }
     check(hipEventCreateWithFlags(&h->ev_join[0], kSyncEvent), "hipEventCreateWithFlags");
     check(hipEventCreateWithFlags(&h->ev_join[1], kSyncEvent), "hipEventCreateWithFlags");
     {
@@ -677,6 +699,7 @@ int mbots_destroy(mbots_handle *h)
     for (auto e : h->pool) (void)hipEventDestroy(e);
     if (h->ev_totals) (void)hipEventDestroy(h->ev_totals);
     if (h->ev_hop) (void)hipEventDestroy(h->ev_hop);
+    if (h->sig_fork) (void)hipFree(h->sig_fork);
     for (auto e : h->ev_join) if (e) (void)hipEventDestroy(e);
     if (h->aux) (void)hipStreamDestroy(h->aux);
     if (h->h_totals) (void)hipHostFree(h->h_totals);
@@ -744,16 +767,25 @@ int mbots_step(mbots_handle *h, void *stream)
     // sensor's stream wait on ev_totals, carried by K2's own dispatch
     // (under stream capture -- a caller recording steps into a HIP graph -- the
     // fork / join events are recorded by hipEventRecord, the capturable form)
-    if ((rc = timed(h, MBOTS_TK_SCAN, st,
-                    [&] { return mbots::launch_scan(h->S, par, st, h->ev_totals, capturing); })))
-        return rc;
+    // the fork by value (small world counts, eagerly): K2's last block raises
+    // this step's epoch (under capture replays would repeat it: the event then)
+    uint32_t epoch = 0;
+    if (h->sig_fork && !capturing) {
+        if (++h->epoch == 0) ++h->epoch;
+        epoch = h->epoch;
+    }
+    h->S.epoch = epoch;
+    rc = timed(h, MBOTS_TK_SCAN, st, [&] { return mbots::launch_scan(h->S, par, st, h->ev_totals, capturing); });
+    h->S.epoch = 0;
+    if (rc) return rc;
     // fork after K2: the K3b sensor (VALU-bound; it derives the export rows from
     // K2's row_base itself) runs on the aux stream while this stream goes on
     // with K3a export, shift_observations and the learner's action writes --
     // none of which reads the sensor rows or the finder slots.  The next step's
     // K1 and the semantic/depth accessors wait for ev_join.
     const int jcur = h->last_join == 0 ? 1 : 0;
-    HIP_TRY(hipStreamWaitEvent(h->aux, h->ev_totals, 0));
+    if (epoch) HIP_TRY(hipStreamWaitValue32(h->aux, h->sig_fork, epoch, hipStreamWaitValueEq, 0xFFFFFFFFu));
+    else HIP_TRY(hipStreamWaitEvent(h->aux, h->ev_totals, 0));
     if ((rc = timed(h, MBOTS_TK_SENSOR, h->aux, [&] {
              return mbots::launch_sensor(h->S, nxt, h->aux, h->ev_join[jcur], capturing);
          })))
