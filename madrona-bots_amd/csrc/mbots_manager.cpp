@@ -645,10 +645,15 @@ int mbots_create(const mbots_config *cfg_in, mbots_handle **out)
     constexpr unsigned kSyncEvent = hipEventDisableTiming | hipEventReleaseToDevice;
     check(hipEventCreateWithFlags(&h->ev_totals, kSyncEvent), "hipEventCreateWithFlags");
     check(hipEventCreateWithFlags(&h->ev_hop, kSyncEvent), "hipEventCreateWithFlags");
-    if (fork_by_value((uint32_t)S.W)) {
-        // the word hipStreamWaitValue32 polls (read by the command processor)
-        check(hipExtMallocWithFlags((void **)&h->sig_fork, 8, hipMallocSignalMemory), "hipExtMallocWithFlags");
-        if (rc == MBOTS_OK) check(hipMemset(h->sig_fork, 0, 8), "hipMemset");
+    if (rc == MBOTS_OK && fork_by_value((uint32_t)S.W)) {
+        // the word hipStreamWaitValue32 polls (the runtime's wait kernel reads
+        // it); without signal memory the fork stays an event wait
+        if (hipExtMallocWithFlags((void **)&h->sig_fork, 8, hipMallocSignalMemory) != hipSuccess) {
+            (void)hipGetLastError();
+            h->sig_fork = nullptr;
+        } else {
+            check(hipMemset(h->sig_fork, 0, 8), "hipMemset");
+        }
         S.sig_fork = h->sig_fork;
     }
     check(hipEventCreateWithFlags(&h->ev_join[0], kSyncEvent), "hipEventCreateWithFlags");
