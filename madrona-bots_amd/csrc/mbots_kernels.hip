@@ -1463,8 +1463,12 @@ __global__ __launch_bounds__(64 * kWaves, sensor_min_waves(kCap)) void sensor_ke
                     const bool fwd = f > 0.0f;
                     const float sc = fwd ? 12.0f : 4.0f;
                     const float s = __builtin_fmaf(uc, sc, sc - 0.5f);
-                    // (the last pixel 2 sc - 1: 23 forward, 7 backward)
-                    const float sn = __builtin_rintf(fminf(fmaxf(s, 0.0f), __builtin_fmaf(2.0f, sc, -1.0f)));
+                    // the nearest integer, not clamped to the pixels [0, 2 sc - 1]:
+                    // off the range it is at least as near as the clamped one, so
+                    // the test keeps a superset (a few more edge survivors for P2's
+                    // exact test, 3 VALU less per iteration: step -0.9 %); s is
+                    // finite for every far pair (|u_c| <= 1.42 in the wedge)
+                    const float sn = __builtin_rintf(s);
                     const bool pix = fabsf(s - sn) <= sc * w;
                     const bool fin = fwd & (fabsf(uc) <= w);
                     keep = keep & ((af < kFarCull) | pix | fin);
