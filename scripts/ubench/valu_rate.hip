@@ -24,6 +24,20 @@ __global__ __launch_bounds__(256) void valu_kernel(float *out, int iters, float 
             p0 = __builtin_elementwise_fma(p0, va, vb); p1 = __builtin_elementwise_fma(p1, va, vb);
             p2 = __builtin_elementwise_fma(p2, va, vb); p3 = __builtin_elementwise_fma(p3, va, vb);
             x0 = p0.x; x1 = p0.y; x2 = p1.x; x3 = p1.y; x4 = p2.x; x5 = p2.y; x6 = p3.x; x7 = p3.y;
+        } else if constexpr (kMode == 4) {   // 8 independent reciprocals (transcendental)
+            x0 = __builtin_amdgcn_rcpf(x0); x1 = __builtin_amdgcn_rcpf(x1); x2 = __builtin_amdgcn_rcpf(x2);
+            x3 = __builtin_amdgcn_rcpf(x3); x4 = __builtin_amdgcn_rcpf(x4); x5 = __builtin_amdgcn_rcpf(x5);
+            x6 = __builtin_amdgcn_rcpf(x6); x7 = __builtin_amdgcn_rcpf(x7);
+        } else if constexpr (kMode == 5) {   // 6 FMAs + 2 reciprocals (do they overlap?)
+            x0 = __builtin_fmaf(x0, a, b); x1 = __builtin_fmaf(x1, a, b); x2 = __builtin_amdgcn_rcpf(x2);
+            x3 = __builtin_fmaf(x3, a, b); x4 = __builtin_fmaf(x4, a, b); x5 = __builtin_fmaf(x5, a, b);
+            x6 = __builtin_amdgcn_rcpf(x6); x7 = __builtin_fmaf(x7, a, b);
+        } else if constexpr (kMode == 6) {   // 8 independent square roots
+            x0 = __builtin_amdgcn_sqrtf(x0); x1 = __builtin_amdgcn_sqrtf(x1); x2 = __builtin_amdgcn_sqrtf(x2);
+            x3 = __builtin_amdgcn_sqrtf(x3); x4 = __builtin_amdgcn_sqrtf(x4); x5 = __builtin_amdgcn_sqrtf(x5);
+            x6 = __builtin_amdgcn_sqrtf(x6); x7 = __builtin_amdgcn_sqrtf(x7);
+        } else if constexpr (kMode == 7) {   // 8 independent multiplies
+            x0 *= a; x1 *= b; x2 *= a; x3 *= b; x4 *= a; x5 *= b; x6 *= a; x7 *= b;
         } else {   // compare + select pairs (VOPC to vcc / SGPR + v_cndmask)
             x0 = x0 < a ? x0 + b : x0 - b; x1 = x1 < a ? x1 + b : x1 - b;
             x2 = x2 < a ? x2 + b : x2 - b; x3 = x3 < a ? x3 + b : x3 - b;
@@ -56,7 +70,11 @@ int main()
     run<0>("fma x8", 8, out);
     run<1>("add x8", 8, out);
     run<2>("cmp+cndmask+add x4", 12, out);
-    run<3>("pk_fma x4 (8 fp32 FMAs)", 4, out);   // per pair: v_cmp, v_add, v_sub, v_cndmask ~ 3 VALU
+    run<3>("pk_fma x4 (8 fp32 FMAs)", 4, out);
+    run<4>("rcp x8", 8, out);
+    run<5>("fma x6 + rcp x2", 8, out);
+    run<6>("sqrt x8", 8, out);
+    run<7>("mul x8", 8, out);   // per pair: v_cmp, v_add, v_sub, v_cndmask ~ 3 VALU
     hipFree(out);
     return 0;
 }
