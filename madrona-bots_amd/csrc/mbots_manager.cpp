@@ -20,6 +20,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <new>
@@ -128,7 +129,24 @@ namespace {
 #ifndef MB_VALUE_FORK_MAX
 #define MB_VALUE_FORK_MAX 8192
 #endif
-bool fork_by_value(uint32_t W) { return W <= MB_VALUE_FORK_MAX; }
+// The runtime carries the wait as a polling kernel on the sensor's queue, which
+// spins until K2 (on the caller's queue) raises the flag: under a tool that runs
+// the device's kernels one at a time (rocprofv3 counter collection,
+// AMD_SERIALIZE_KERNEL) the poller can be dispatched first and never end, so
+// those keep the event wait (as does MBOTS_VALUE_FORK=0).
+bool env_set(const char *name)
+{
+    const char *v = std::getenv(name);
+    return v && *v && std::strcmp(v, "0") != 0;
+}
+bool fork_by_value(uint32_t W)
+{
+    if (W > MB_VALUE_FORK_MAX) return false;
+    const char *o = std::getenv("MBOTS_VALUE_FORK");
+    if (o && std::strcmp(o, "0") == 0) return false;
+    return !(env_set("ROCPROF_COUNTER_COLLECTION") || env_set("AMD_SERIALIZE_KERNEL") ||
+             env_set("HSA_TOOLS_LIB") || env_set("ROCP_INPUT"));
+}
 
 hipEvent_t get_event(mbots_handle *h)
 {
