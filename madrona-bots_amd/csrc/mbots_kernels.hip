@@ -2138,6 +2138,20 @@ hipError_t launch_init(const SimState &S, hipStream_t st)
     hipLaunchKernelGGL(init_kernel, dim3(world_blocks(S.W)), dim3(256), 0, st, S);
     return hipGetLastError();
 }
+// the join as a value wait (small world counts, mbots_step): one wave after the
+// sensor on its queue stores the step's epoch (a vector store at system scope)
+// into the signal word the next step's K1 queue polls
+__global__ __launch_bounds__(64) void raise_flag_kernel(uint32_t *flag, uint32_t v)
+{
+    if (threadIdx.x == 0) __hip_atomic_store(flag, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+hipError_t launch_raise_flag(uint32_t *flag, uint32_t v, hipStream_t st)
+{
+    hipLaunchKernelGGL(raise_flag_kernel, dim3(1), dim3(64), 0, st, flag, v);
+    return hipGetLastError();
+}
+
 hipError_t launch_tile_sum(const SimState &S, int parity, hipStream_t st)
 {
     hipLaunchKernelGGL(tile_sum_kernel, dim3(S.ntiles), dim3(1024), 0, st, S, parity);

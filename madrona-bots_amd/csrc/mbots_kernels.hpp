@@ -87,6 +87,7 @@ hipError_t launch_init(const SimState &S, hipStream_t st);
 // the sensor's ray table (host-computed with the kernels' own u_of / near_pt)
 hipError_t upload_ray_table(const SimState &S, hipStream_t st);
 hipError_t launch_tile_sum(const SimState &S, int parity, hipStream_t st);
+hipError_t launch_raise_flag(uint32_t *flag, uint32_t v, hipStream_t st);
 hipError_t launch_world_step(const SimState &S, const ObsTable &cur, int parity, hipStream_t st);
 // plain_events: record `done` with hipEventRecord (stream capture) instead of on the dispatch
 hipError_t launch_scan(const SimState &S, int parity, hipStream_t st, hipEvent_t done = nullptr,

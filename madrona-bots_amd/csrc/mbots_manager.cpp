@@ -102,7 +102,10 @@ struct mbots_handle {
                                           // still its current ones (lazy shift, K5)
     hipEvent_t ev_hop = nullptr;      // orders a call's stream after the last one used
     uint32_t *sig_fork = nullptr;     // the fork's signal word (small world counts)
+    uint32_t *sig_join = nullptr;     // the join's (raised after the sensor)
     uint32_t epoch = 0;               // the last epoch K2 raised (never 0)
+    uint32_t join_epoch = 0;          // the epoch raised after the last sensor (0: none;
+                                      // the join is then the sensor's event)
     bool totals_ok = false;           // h_totals holds the last step's counts (synchronised)
     int forced = 0;                   // deferred parts the caller's reads needed since the
                                       // last step (kMove*): the next step prefetches them
@@ -129,6 +132,12 @@ namespace {
 #ifndef MB_VALUE_FORK_MAX
 #define MB_VALUE_FORK_MAX 8192
 #endif
+#ifndef MB_VALUE_JOIN
+#define MB_VALUE_JOIN 1   // the join too: a one-wave kernel after the sensor raises it
+#endif
+#ifndef MB_VALUE_JOIN_MAX
+#define MB_VALUE_JOIN_MAX 8192
+#endif
 // The runtime carries the wait as a polling kernel on the sensor's queue, which
 // spins until K2 (on the caller's queue) raises the flag: under a tool that runs
 // the device's kernels one at a time (rocprofv3 counter collection,
@@ -139,14 +148,15 @@ bool env_set(const char *name)
     const char *v = std::getenv(name);
     return v && *v && std::strcmp(v, "0") != 0;
 }
-bool fork_by_value(uint32_t W)
+bool value_waits_safe()
 {
-    if (W > MB_VALUE_FORK_MAX) return false;
     const char *o = std::getenv("MBOTS_VALUE_FORK");
     if (o && std::strcmp(o, "0") == 0) return false;
     return !(env_set("ROCPROF_COUNTER_COLLECTION") || env_set("AMD_SERIALIZE_KERNEL") ||
              env_set("HSA_TOOLS_LIB") || env_set("ROCP_INPUT"));
 }
+bool fork_by_value(uint32_t W) { return W <= MB_VALUE_FORK_MAX && value_waits_safe(); }
+bool join_by_value(uint32_t W) { return MB_VALUE_JOIN && W <= MB_VALUE_JOIN_MAX && value_waits_safe(); }
 
 hipEvent_t get_event(mbots_handle *h)
 {
@@ -663,15 +673,20 @@ int mbots_create(const mbots_config *cfg_in, mbots_handle **out)
     constexpr unsigned kSyncEvent = hipEventDisableTiming | hipEventReleaseToDevice;
     check(hipEventCreateWithFlags(&h->ev_totals, kSyncEvent), "hipEventCreateWithFlags");
     check(hipEventCreateWithFlags(&h->ev_hop, kSyncEvent), "hipEventCreateWithFlags");
-    if (rc == MBOTS_OK && fork_by_value((uint32_t)S.W)) {
-        // the word hipStreamWaitValue32 polls (the runtime's wait kernel reads
-        // it); without signal memory the fork stays an event wait
-        if (hipExtMallocWithFlags((void **)&h->sig_fork, 8, hipMallocSignalMemory) != hipSuccess) {
-            (void)hipGetLastError();
-            h->sig_fork = nullptr;
-        } else {
-            check(hipMemset(h->sig_fork, 0, 8), "hipMemset");
-        }
+    {
+        // the words hipStreamWaitValue32 polls (the runtime's wait kernel reads
+        // them); without signal memory the waits stay event waits
+        auto signal_word = [&](uint32_t *&p) {
+            if (rc != MBOTS_OK) return;
+            if (hipExtMallocWithFlags((void **)&p, 8, hipMallocSignalMemory) != hipSuccess) {
+                (void)hipGetLastError();
+                p = nullptr;
+                return;
+            }
+            check(hipMemset(p, 0, 8), "hipMemset");
+        };
+        if (fork_by_value((uint32_t)S.W)) signal_word(h->sig_fork);
+        if (join_by_value((uint32_t)S.W)) signal_word(h->sig_join);
         S.sig_fork = h->sig_fork;
     }
     check(hipEventCreateWithFlags(&h->ev_join[0], kSyncEvent), "hipEventCreateWithFlags");
@@ -723,6 +738,7 @@ int mbots_destroy(mbots_handle *h)
     if (h->ev_totals) (void)hipEventDestroy(h->ev_totals);
     if (h->ev_hop) (void)hipEventDestroy(h->ev_hop);
     if (h->sig_fork) (void)hipFree(h->sig_fork);
+    if (h->sig_join) (void)hipFree(h->sig_join);
     for (auto e : h->ev_join) if (e) (void)hipEventDestroy(e);
     if (h->aux) (void)hipStreamDestroy(h->aux);
     if (h->h_totals) (void)hipHostFree(h->h_totals);
@@ -780,7 +796,10 @@ int mbots_step(mbots_handle *h, void *stream)
     // state half that sensor read; the halves swap after K1.
     // (under stream capture only a join recorded in the same capture is waited
     // for: a replay starts after the previous launch of the graph completed)
-    if (h->last_join >= 0 && (!capturing || h->join_capture == cap_id))
+    // (small world counts, eagerly: the flag a wave after the sensor raised)
+    if (!capturing && h->join_epoch != 0)
+        HIP_TRY(hipStreamWaitValue32(st, h->sig_join, h->join_epoch, hipStreamWaitValueEq, 0xFFFFFFFFu));
+    else if (h->last_join >= 0 && (!capturing || h->join_capture == cap_id))
         HIP_TRY(hipStreamWaitEvent(st, h->ev_join[h->last_join], 0));
     if ((rc = timed(h, MBOTS_TK_WORLD_STEP, st,
                     [&] { return mbots::launch_world_step(h->S, cur, par, st); })))
@@ -793,11 +812,11 @@ int mbots_step(mbots_handle *h, void *stream)
     // the fork by value (small world counts, eagerly): K2's last block raises
     // this step's epoch (under capture replays would repeat it: the event then)
     uint32_t epoch = 0;
-    if (h->sig_fork && !capturing) {
+    if ((h->sig_fork || h->sig_join) && !capturing) {
         if (++h->epoch == 0) ++h->epoch;
         epoch = h->epoch;
     }
-    h->S.epoch = epoch;
+    h->S.epoch = h->sig_fork ? epoch : 0u;
     rc = timed(h, MBOTS_TK_SCAN, st, [&] { return mbots::launch_scan(h->S, par, st, h->ev_totals, capturing); });
     h->S.epoch = 0;
     if (rc) return rc;
@@ -807,7 +826,7 @@ int mbots_step(mbots_handle *h, void *stream)
     // none of which reads the sensor rows or the finder slots.  The next step's
     // K1 and the semantic/depth accessors wait for ev_join.
     const int jcur = h->last_join == 0 ? 1 : 0;
-    if (epoch) HIP_TRY(hipStreamWaitValue32(h->aux, h->sig_fork, epoch, hipStreamWaitValueEq, 0xFFFFFFFFu));
+    if (epoch && h->sig_fork) HIP_TRY(hipStreamWaitValue32(h->aux, h->sig_fork, epoch, hipStreamWaitValueEq, 0xFFFFFFFFu));
     else HIP_TRY(hipStreamWaitEvent(h->aux, h->ev_totals, 0));
     if ((rc = timed(h, MBOTS_TK_SENSOR, h->aux, [&] {
              return mbots::launch_sensor(h->S, nxt, h->aux, h->ev_join[jcur], capturing);
@@ -815,6 +834,11 @@ int mbots_step(mbots_handle *h, void *stream)
         return rc;
     h->last_join = jcur;
     h->join_capture = capturing ? cap_id : 0;
+    h->join_epoch = 0;
+    if (epoch && h->sig_join) {
+        HIP_TRY(mbots::launch_raise_flag(h->sig_join, epoch, h->aux));
+        h->join_epoch = epoch;
+    }
     if ((rc = timed(h, MBOTS_TK_EXPORT, st,
                     [&] { return mbots::launch_export_rows(h->S, nxt, 0, st); })))
         return rc;
@@ -1388,6 +1412,7 @@ int mbots_load_checkpoint(mbots_handle *h, const void *src, uint64_t bytes)
     h->tb = 0;
     h->parity = 0;
     h->last_join = -1;
+    h->join_epoch = 0;
     h->prev_lazy[0] = h->prev_lazy[1] = false;
     h->ah_pending[0] = h->ah_pending[1] = false;
     h->six_pending[0] = h->six_pending[1] = false;
