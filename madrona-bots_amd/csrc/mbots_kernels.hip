@@ -2229,7 +2229,16 @@ hipError_t launch_move(const SimState &S, const ObsTable &cur, const ObsTable &n
     // blocks per segment: a launch of few segments (the prev sensor alone, the
     // fused shift with or without the prev sensor) still needs enough waves in
     // flight to stream
-    const unsigned bx = k <= 4 ? (unsigned)MB_MOVE_BLOCKS : 512u;
+    // (at small world counts a block per two worlds covers every item of a
+    // segment in about one pass; more would be empty blocks to dispatch)
+#ifndef MB_MOVE_SMALL
+#define MB_MOVE_SMALL 1
+#endif
+    const unsigned full = k <= 4 ? (unsigned)MB_MOVE_BLOCKS : 512u;
+#ifndef MB_MOVE_SMALL_DIV
+#define MB_MOVE_SMALL_DIV 2
+#endif
+    const unsigned bx = MB_MOVE_SMALL ? std::max(256u, std::min(full, S.W / MB_MOVE_SMALL_DIV)) : full;
     if (parts & kMoveAHShift)
         hipLaunchKernelGGL(shift_move_kernel, dim3(bx, k), dim3(256), 0, st, S.totals, S.src_of, m);
     else
