@@ -138,6 +138,9 @@ namespace {
 #ifndef MB_VALUE_JOIN_MAX
 #define MB_VALUE_JOIN_MAX 8192
 #endif
+#ifndef MB_VALUE_ADAPT
+#define MB_VALUE_ADAPT 1   // value waits only while the host runs ahead of the device
+#endif
 // The runtime carries the wait as a polling kernel on the sensor's queue, which
 // spins until K2 (on the caller's queue) raises the flag: under a tool that runs
 // the device's kernels one at a time (rocprofv3 counter collection,
@@ -796,8 +799,19 @@ int mbots_step(mbots_handle *h, void *stream)
     // state half that sensor read; the halves swap after K1.
     // (under stream capture only a join recorded in the same capture is waited
     // for: a replay starts after the previous launch of the graph completed)
-    // (small world counts, eagerly: the flag a wave after the sensor raised)
-    if (!capturing && h->join_epoch != 0)
+    // (small world counts, eagerly, while the device still runs the previous
+    // step: the flag a wave after the sensor raised.  A host that arrives after
+    // the sensor has finished -- a host-bound loop, where the value waits'
+    // extra enqueues would only add host time -- takes the event wait, and this
+    // step raises no flags.)
+    bool ahead = false;
+    if (!capturing && (h->sig_fork || h->sig_join) && MB_VALUE_ADAPT) {
+        ahead = h->last_join < 0 || hipEventQuery(h->ev_join[h->last_join]) == hipErrorNotReady;
+        (void)hipGetLastError();   // (hipEventQuery reports "not ready" as an error)
+    } else if (!capturing && (h->sig_fork || h->sig_join)) {
+        ahead = true;
+    }
+    if (!capturing && h->join_epoch != 0 && ahead)
         HIP_TRY(hipStreamWaitValue32(st, h->sig_join, h->join_epoch, hipStreamWaitValueEq, 0xFFFFFFFFu));
     else if (h->last_join >= 0 && (!capturing || h->join_capture == cap_id))
         HIP_TRY(hipStreamWaitEvent(st, h->ev_join[h->last_join], 0));
@@ -812,7 +826,7 @@ int mbots_step(mbots_handle *h, void *stream)
     // the fork by value (small world counts, eagerly): K2's last block raises
     // this step's epoch (under capture replays would repeat it: the event then)
     uint32_t epoch = 0;
-    if ((h->sig_fork || h->sig_join) && !capturing) {
+    if ((h->sig_fork || h->sig_join) && !capturing && ahead) {
         if (++h->epoch == 0) ++h->epoch;
         epoch = h->epoch;
     }

@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 #include <hip/hip_ext.h>
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <vector>
 
@@ -141,6 +142,28 @@ int main()
         }
         CK(hipMemcpy(&total_bad, bad, 4, hipMemcpyDeviceToHost));
         printf("{\"mode\": \"coherence after a value wait\", \"stale_words\": %u, \"rounds\": 200}\n", total_bad);
+    }
+    // host cost of the enqueue calls themselves (the flag already set, the
+    // event already fired): what a host-bound loop pays per call
+    {
+        const int n = 2000;
+        auto host_us = [&](auto &&call) -> double {
+            (void)hipDeviceSynchronize();
+            const auto t0 = std::chrono::steady_clock::now();
+            for (int i = 0; i < n; ++i) call();
+            const auto t1 = std::chrono::steady_clock::now();
+            (void)hipDeviceSynchronize();
+            return std::chrono::duration<double, std::micro>(t1 - t0).count() / n;
+        };
+        CK(hipEventRecord(ev, s1));
+        const double u_launch = host_us([&] { hipLaunchKernelGGL(kern_b, dim3(1), dim3(64), 0, s2, t + 2); });
+        const double u_ext = host_us([&] {
+            hipExtLaunchKernelGGL(kern_b, dim3(1), dim3(64), 0, s2, nullptr, ev, 0u, t + 2);
+        });
+        const double u_wev = host_us([&] { (void)hipStreamWaitEvent(s2, ev, 0); });
+        const double u_wval = host_us([&] { (void)hipStreamWaitValue32(s2, flag, epoch, hipStreamWaitValueEq, 0xFFFFFFFFu); });
+        printf("{\"mode\": \"host us per enqueue\", \"launch\": %.2f, \"ext_launch_with_event\": %.2f, "
+               "\"wait_event\": %.2f, \"wait_value32\": %.2f}\n", u_launch, u_ext, u_wev, u_wval);
     }
     return 0;
 }
