@@ -36,11 +36,22 @@ constexpr int kTileWorlds = 1024;             // worlds per scan tile (K2 block)
 #endif
 #ifndef MB_NT
 #define MB_NT 35  // non-temporal stores: 1 K4, 2 K5, 4 K3a, 8 sensor output;
-                  // non-temporal loads: 32 K4 sources, 64 K5 sources;
-                  // 128: K1 compaction stores
+                  // non-temporal loads: 32 K4 sources, 64 K5 sources
 #endif
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+// a 4-byte store written through to memory (MB_WT: system scope, the L2 keeps
+// no dirty copy; else a plain store)
+#ifndef MB_WT
+#define MB_WT 1
+#endif
+template <typename T>
+__device__ __forceinline__ void st_wt(T *p, T v)
+{
+    static_assert(sizeof(T) == 4, "4-byte columns");
+    if (MB_WT) __hip_atomic_store(reinterpret_cast<uint32_t *>(p), __builtin_bit_cast(uint32_t, v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    else *p = v;
+}
 __device__ __forceinline__ void st_stream(uint32_t *p, uint32_t v, bool nt)
 {
     if (nt) __builtin_nontemporal_store(v, p);
@@ -547,17 +558,19 @@ __device__ void world_step(SimState &S, const ObsTable &cur, WorldLDS<kCap> &L, 
         const uint64_t m = ballot64(alive);
         if (alive) {
             const size_t d = base + nn + rank_below(m);
-            constexpr bool nt = (MB_NT & 128) != 0;
-            st_stream(S.x_out + d, L.x[i], nt);
-            st_stream(S.y_out + d, L.y[i], nt);
-            st_stream(S.rw_out + d, L.rw[i], nt);
-            st_stream(S.rz_out + d, L.rz[i], nt);
-            st_stream(S.species_out + d, (int32_t)L.species[i], nt);
-            st_stream(S.health + d, L.accum[i], nt);
-            st_stream(S.obsrow_out + d, i < n0 ? rows[g] : -1, nt);   // newborns: no row
-            st_stream(S.sur0 + d, L.sur0[i], nt);
-            st_stream(S.sur1 + d, L.sur1[i], nt);
-            st_stream(S.stats + d, (uint32_t)(L.flags[i] & F_STATS), nt);
+            // write-through (system-scope vector stores): no dirty lines left
+            // for the end-of-kernel write-back, which K2 waits for (-1.5 % at
+            // 4096 worlds, where the step is that latency chain; +-0 at 65536)
+            st_wt(S.x_out + d, L.x[i]);
+            st_wt(S.y_out + d, L.y[i]);
+            st_wt(S.rw_out + d, L.rw[i]);
+            st_wt(S.rz_out + d, L.rz[i]);
+            st_wt(S.species_out + d, (int32_t)L.species[i]);
+            st_wt(S.health + d, L.accum[i]);
+            st_wt(S.obsrow_out + d, i < n0 ? rows[g] : -1);   // newborns: no row
+            st_wt(S.sur0 + d, L.sur0[i]);
+            st_wt(S.sur1 + d, L.sur1[i]);
+            st_wt(S.stats + d, (uint32_t)(L.flags[i] & F_STATS));
             atomicAdd(&L.scount[L.species[i] - 1], 1);
         }
         nn += __popcll(m);
