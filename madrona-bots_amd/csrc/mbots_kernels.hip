@@ -2242,16 +2242,20 @@ hipError_t launch_move(const SimState &S, const ObsTable &cur, const ObsTable &n
     // blocks per segment: a launch of few segments (the prev sensor alone, the
     // fused shift with or without the prev sensor) still needs enough waves in
     // flight to stream
-    // (at small world counts a block per two worlds covers every item of a
-    // segment in about one pass; more would be empty blocks to dispatch)
+    // (below 16384 worlds a block per two worlds, at most 2048 per segment,
+    // covers a segment's items in one or two passes; more would be mostly
+    // empty blocks holding wave slots the sensor beside it needs:
+    // profiles/r04_shift_grid_small_ab.jsonl, r04_shift_grid_cap_ab.jsonl)
 #ifndef MB_MOVE_SMALL
 #define MB_MOVE_SMALL 1
 #endif
-    const unsigned full = k <= 4 ? (unsigned)MB_MOVE_BLOCKS : 512u;
-#ifndef MB_MOVE_SMALL_DIV
-#define MB_MOVE_SMALL_DIV 2
+#ifndef MB_MOVE_SMALL_CAP
+#define MB_MOVE_SMALL_CAP 2048u
 #endif
-    const unsigned bx = MB_MOVE_SMALL ? std::max(256u, std::min(full, S.W / MB_MOVE_SMALL_DIV)) : full;
+    const unsigned full = k <= 4 ? (unsigned)MB_MOVE_BLOCKS : 512u;
+    const unsigned bx = MB_MOVE_SMALL && S.W < 16384u
+                            ? std::max(256u, std::min(std::min(full, (unsigned)MB_MOVE_SMALL_CAP), S.W / 2u))
+                            : full;
     if (parts & kMoveAHShift)
         hipLaunchKernelGGL(shift_move_kernel, dim3(bx, k), dim3(256), 0, st, S.totals, S.src_of, m);
     else
