@@ -2242,7 +2242,7 @@ hipError_t launch_move(const SimState &S, const ObsTable &cur, const ObsTable &n
     // blocks per segment: a launch of few segments (the prev sensor alone, the
     // fused shift with or without the prev sensor) still needs enough waves in
     // flight to stream
-    // (below 16384 worlds a block per two worlds, at most 2048 per segment,
+    // (below 65536 worlds a block per two worlds, at most 2048 per segment,
     // covers a segment's items in one or two passes; more would be mostly
     // empty blocks holding wave slots the sensor beside it needs:
     // profiles/r04_shift_grid_small_ab.jsonl, r04_shift_grid_cap_ab.jsonl)
@@ -2253,7 +2253,7 @@ hipError_t launch_move(const SimState &S, const ObsTable &cur, const ObsTable &n
 #define MB_MOVE_SMALL_CAP 2048u
 #endif
     const unsigned full = k <= 4 ? (unsigned)MB_MOVE_BLOCKS : 512u;
-    const unsigned bx = MB_MOVE_SMALL && S.W < 16384u
+    const unsigned bx = MB_MOVE_SMALL && S.W < 65536u
                             ? std::max(256u, std::min(std::min(full, (unsigned)MB_MOVE_SMALL_CAP), S.W / 2u))
                             : full;
     if (parts & kMoveAHShift)
