@@ -250,6 +250,11 @@ int mbots_write_synthetic_actions(mbots_handle *h, uint32_t seed, uint32_t step,
  * does this itself; a caller recording steps into a HIP graph (stream capture)
  * ends the captured sequence with it, so the capture has no unjoined work. */
 int mbots_join(mbots_handle *h, void *stream);
+/* Record `event` (a hipEvent_t, timing-enabled) on the internal stream after
+ * the last step's sensor: a timing point for benchmarks that adds no wait to
+ * any stream (bench.py's device span: the later of this and an event on the
+ * caller's stream).  No step yet, or CPU mode: MBOTS_E_INVALID. */
+int mbots_record_sensor_done(mbots_handle *h, void *event);
 /* running total of agent-steps (sum over steps of live agents after the step) */
 int mbots_agent_steps(mbots_handle *h, uint64_t *out);
 /* births/respawns dropped because a world reached agent_capacity */

@@ -1301,6 +1301,15 @@ int mbots_join(mbots_handle *h, void *stream)
     return MBOTS_OK;
 }
 
+int mbots_record_sensor_done(mbots_handle *h, void *event)
+{
+    if (!h || !event) return fail(MBOTS_E_INVALID, "null argument");
+    if (h->cpu || h->last_join < 0) return fail(MBOTS_E_INVALID, "no sensor launched on the device");
+    HIP_TRY(hipSetDevice(h->device));
+    HIP_TRY(hipEventRecord(static_cast<hipEvent_t>(event), h->aux));
+    return MBOTS_OK;
+}
+
 int mbots_agent_steps(mbots_handle *h, uint64_t *out)
 {
     if (!h || !out) return fail(MBOTS_E_INVALID, "null argument");

@@ -75,6 +75,7 @@ def _load():
         "mbots_agent_offset_for_world": [vp, u32, P(u32)],
         "mbots_write_synthetic_actions": [vp, u32, u32, i32, vp],
         "mbots_join": [vp, vp],
+        "mbots_record_sensor_done": [vp, vp],
         "mbots_rollout_record_bytes": [vp, P(u32)],
         "mbots_pack_rollout": [vp, vp, ctypes.c_uint64, vp],
         "mbots_unpack_rollout": [vp, ctypes.c_uint64, i32, i32, vp, vp, vp, vp],
@@ -579,6 +580,14 @@ class SimManager:
         sensor work (mbots_join): ends a sequence of steps captured into a
         HIP graph (torch.cuda.graph) with no unjoined work."""
         _check(_lib.mbots_join(self._h, self._stream()))
+
+    def record_sensor_done(self, event):
+        """Record a timing-enabled torch.cuda.Event on the manager's internal
+        stream after the last step's sensor (mbots_record_sensor_done): a
+        benchmark timing point that adds no wait to any stream."""
+        if not event.cuda_event:   # torch creates its events on first record
+            event.record()
+        _check(_lib.mbots_record_sensor_done(self._h, ctypes.c_void_p(event.cuda_event)))
 
     def write_synthetic_actions(self, seed, step, write_hidden=False):
         _check(_lib.mbots_write_synthetic_actions(self._h, int(seed) & 0xFFFFFFFF,
