@@ -1041,6 +1041,29 @@ __host__ __device__ constexpr float u_of(int k)
     return k < 24 ? (float)(2 * k - 23) * (1.0f / 24.0f) : (float)(2 * (k - 24) - 7) * 0.125f;
 }
 
+// wave-wide compare masks (VOPC results as 64-bit lane masks; every lane
+// active) and a select by such a mask (v_cndmask on the SGPR pair)
+#ifndef MB_P1_MASKS
+#define MB_P1_MASKS 1
+#endif
+constexpr int kCmpOGT = 2, kCmpOLT = 4, kCmpOLE = 5, kCmpNE = 33, kCmpSLT = 40;
+template <int kPred>
+__device__ __forceinline__ uint64_t fcmp_mask(float a, float b)
+{
+    return __builtin_amdgcn_fcmpf(a, b, kPred);
+}
+template <int kPred>
+__device__ __forceinline__ uint64_t icmp_mask(int a, int b)
+{
+    return __builtin_amdgcn_uicmp((unsigned)a, (unsigned)b, kPred);
+}
+__device__ __forceinline__ int select_by_mask(uint64_t m, int if_set, int if_clear)
+{
+    int r;
+    asm volatile("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(if_clear), "v"(if_set), "s"(m));
+    return r;
+}
+
 // (f, l) of object j in agent i's frame; order of the object (food at
 // [0, nf), agents from na = nf rounded up to 8; the gap holds NaN, which no
 // queued pair references, so j < na tells food from agents)
@@ -1486,10 +1509,36 @@ __global__ __launch_bounds__(64 * kWaves, sensor_min_waves(kCap)) void sensor_ke
                     const bool fin = fwd & (fabsf(uc) <= w);
                     keep = keep & ((af < kFarCull) | pix | fin);
                 }
+#if MB_P1_MASKS
+                // the keep mask straight from the compares (P1 runs with every
+                // lane active): VOPC masks combined by scalar ops, and the queue
+                // slot selected by the mask itself -- no per-lane bool turned
+                // back into a ballot (2 VALU less per iteration)
+                (void)keep;
+                uint64_t m = fcmp_mask<kCmpOLE>(fabsf(l), af + wk);
+                if (!kPad) m &= icmp_mask<kCmpSLT>(j, nobj);
+                if (kKind != 0) m &= icmp_mask<kCmpNE>(j, self);
+                {
+                    const float rf = __builtin_amdgcn_rcpf(f);
+                    const float uc = l * rf;
+                    const float ar = rk * fabsf(rf);
+                    const float w = __builtin_fmaf(
+                        ar, __builtin_fmaf(ar, __builtin_fmaf(2.9f, ar, fabsf(uc)), __builtin_fmaf(0.5f * uc, uc, 1.0f)),
+                        1e-4f);
+                    const float sc = f > 0.0f ? 12.0f : 4.0f;
+                    const float s = __builtin_fmaf(uc, sc, sc - 0.5f);
+                    const float sn = __builtin_rintf(s);
+                    m &= fcmp_mask<kCmpOLT>(af, kFarCull) | fcmp_mask<kCmpOLE>(fabsf(s - sn), sc * w) |
+                         (fcmp_mask<kCmpOGT>(f, 0.0f) & fcmp_mask<kCmpOLE>(fabsf(uc), w));
+                }
+                L.qcode[select_by_mask(m, nq + (int)rank_below(m), kQueueCap)] = (uint32_t)a | ((uint32_t)j << 11);
+                nq += __popcll(m);
+#else
                 const uint64_t m = ballot64(keep);
                 // branch-free: culled lanes write the sink slot (+1 % step)
                 L.qcode[keep ? nq + (int)rank_below(m) : kQueueCap] = (uint32_t)a | ((uint32_t)j << 11);
                 nq += __popcll(m);
+#endif
                 if (nq >= 64) {
                     wave_sync();
 #ifndef MB_SKIP_P2
