@@ -1477,7 +1477,14 @@ __global__ __launch_bounds__(64 * kWaves, sensor_min_waves(kCap)) void sensor_ke
                 const float rk = food ? 1.42f * 1.001f : kAgentR * 1.001f;
                 const float wk = food ? 1.41421356f * (1.42f * 1.001f) + 0.05f
                                       : 1.41421356f * (kAgentR * 1.001f) + 0.05f;
-                bool keep = (kPad | (j < nobj)) & (kKind == 0 || j != self) & (fabsf(l) <= af + wk);
+#if MB_P1_MASKS
+                // the keep mask straight from the compares (P1 runs with every
+                // lane active): VOPC masks combined by scalar ops, and the queue
+                // slot selected by the mask itself -- no per-lane bool turned
+                // back into a ballot (2 VALU less per iteration)
+                uint64_t m = fcmp_mask<kCmpOLE>(fabsf(l), af + wk);
+                if (!kPad) m &= icmp_mask<kCmpSLT>(j, nobj);
+                if (kKind != 0) m &= icmp_mask<kCmpNE>(j, self);
                 {
                     // a far pair (|f| >= kFarCull) also needs a pixel centre, or
                     // forward the finder ray u = 0, within w of its centre's
@@ -1496,8 +1503,7 @@ __global__ __launch_bounds__(64 * kWaves, sensor_min_waves(kCap)) void sensor_ke
                     const float w = __builtin_fmaf(
                         ar, __builtin_fmaf(ar, __builtin_fmaf(2.9f, ar, fabsf(uc)), __builtin_fmaf(0.5f * uc, uc, 1.0f)),
                         1e-4f);
-                    const bool fwd = f > 0.0f;
-                    const float sc = fwd ? 12.0f : 4.0f;
+                    const float sc = f > 0.0f ? 12.0f : 4.0f;
                     const float s = __builtin_fmaf(uc, sc, sc - 0.5f);
                     // the nearest integer, not clamped to the pixels [0, 2 sc - 1]:
                     // off the range it is at least as near as the clamped one, so
@@ -1505,19 +1511,13 @@ __global__ __launch_bounds__(64 * kWaves, sensor_min_waves(kCap)) void sensor_ke
                     // exact test, 3 VALU less per iteration: step -0.9 %); s is
                     // finite for every far pair (|u_c| <= 1.42 in the wedge)
                     const float sn = __builtin_rintf(s);
-                    const bool pix = fabsf(s - sn) <= sc * w;
-                    const bool fin = fwd & (fabsf(uc) <= w);
-                    keep = keep & ((af < kFarCull) | pix | fin);
+                    m &= fcmp_mask<kCmpOLT>(af, kFarCull) | fcmp_mask<kCmpOLE>(fabsf(s - sn), sc * w) |
+                         (fcmp_mask<kCmpOGT>(f, 0.0f) & fcmp_mask<kCmpOLE>(fabsf(uc), w));
                 }
-#if MB_P1_MASKS
-                // the keep mask straight from the compares (P1 runs with every
-                // lane active): VOPC masks combined by scalar ops, and the queue
-                // slot selected by the mask itself -- no per-lane bool turned
-                // back into a ballot (2 VALU less per iteration)
-                (void)keep;
-                uint64_t m = fcmp_mask<kCmpOLE>(fabsf(l), af + wk);
-                if (!kPad) m &= icmp_mask<kCmpSLT>(j, nobj);
-                if (kKind != 0) m &= icmp_mask<kCmpNE>(j, self);
+                L.qcode[select_by_mask(m, nq + (int)rank_below(m), kQueueCap)] = (uint32_t)a | ((uint32_t)j << 11);
+                nq += __popcll(m);
+#else   // (the per-lane form: the same tests as a bool, turned back into a ballot)
+                bool keep = (kPad | (j < nobj)) & (kKind == 0 || j != self) & (fabsf(l) <= af + wk);
                 {
                     const float rf = __builtin_amdgcn_rcpf(f);
                     const float uc = l * rf;
@@ -1525,15 +1525,14 @@ __global__ __launch_bounds__(64 * kWaves, sensor_min_waves(kCap)) void sensor_ke
                     const float w = __builtin_fmaf(
                         ar, __builtin_fmaf(ar, __builtin_fmaf(2.9f, ar, fabsf(uc)), __builtin_fmaf(0.5f * uc, uc, 1.0f)),
                         1e-4f);
-                    const float sc = f > 0.0f ? 12.0f : 4.0f;
+                    const bool fwd = f > 0.0f;
+                    const float sc = fwd ? 12.0f : 4.0f;
                     const float s = __builtin_fmaf(uc, sc, sc - 0.5f);
                     const float sn = __builtin_rintf(s);
-                    m &= fcmp_mask<kCmpOLT>(af, kFarCull) | fcmp_mask<kCmpOLE>(fabsf(s - sn), sc * w) |
-                         (fcmp_mask<kCmpOGT>(f, 0.0f) & fcmp_mask<kCmpOLE>(fabsf(uc), w));
+                    const bool pix = fabsf(s - sn) <= sc * w;
+                    const bool fin = fwd & (fabsf(uc) <= w);
+                    keep = keep & ((af < kFarCull) | pix | fin);
                 }
-                L.qcode[select_by_mask(m, nq + (int)rank_below(m), kQueueCap)] = (uint32_t)a | ((uint32_t)j << 11);
-                nq += __popcll(m);
-#else
                 const uint64_t m = ballot64(keep);
                 // branch-free: culled lanes write the sink slot (+1 % step)
                 L.qcode[keep ? nq + (int)rank_below(m) : kQueueCap] = (uint32_t)a | ((uint32_t)j << 11);
