@@ -48,6 +48,7 @@ VALU_PEAK_INSTR_S = 1024 * 2.4e9 / 2
 SEED = 69                   # learn/env.py:15
 ACTION_SEED = 1234
 AGENTS_PER_WORLD = 32       # learn/env.py:15
+CONFIG4_WORLDS = 262144     # BASELINE config 4 (sharded across 8 GPUs)
 
 
 def algorithmic_bytes(n_agents, n_worlds):
@@ -432,7 +433,8 @@ def main():
     ap.add_argument("--same-device", action="store_true",
                     help="rehearsal: every rank uses cuda:0 (with --backend gloo)")
     ap.add_argument("--no-secondary", action="store_true",
-                    help="skip the reference-loop lines (config 2 at 4096 worlds/GPU, and at --worlds)")
+                    help="skip the secondary lines (config 2 at 4096 worlds/GPU, config 4 at 262144 worlds "
+                         "in all, the reference loop at 4096 worlds/GPU and at --worlds)")
     ap.add_argument("--stream-priority", choices=("high", "normal"), default="high",
                     help="priority of the torch stream the step is launched on (the sensor's internal "
                          "stream is always high): both chains at high priority run the step 1.6 %% "
@@ -441,7 +443,7 @@ def main():
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         # `python bench.py --gpus N` without a launcher: start the N ranks
-        # ourselves (still GPU-free here: only device_count, no HIP context)
+        # ourselves (this parent makes no GPU call at all: spawn_ranks)
         sys.exit(spawn_ranks(args))
     world_size = int(os.environ.get("WORLD_SIZE", "1"))
     if world_size != args.gpus:
@@ -542,11 +544,19 @@ def main():
             cfg5 = config5_loop(mgr, args, rank, world_size, dev, distributed)
         except Exception as e:   # reported in the line; the main measurement stands
             cfg5 = {"error": f"{type(e).__name__}: {e}"[:400]}
-    secondary = ref_main = config2 = None
+    secondary = ref_main = config2 = config4 = None
     if not args.no_secondary:
         config2 = bare_loop(4096, args, rank, world_size, dev, distributed,
                             "BASELINE config 2 on the headline's workload: step + shift + action write at "
                             "4096 worlds/GPU")
+        # BASELINE config 4: 262144 worlds in all, sharded over the ranks
+        # (strong scaling: 262144 / N worlds per GPU; at N = 8 the config itself)
+        if CONFIG4_WORLDS % world_size == 0:
+            config4 = bare_loop(CONFIG4_WORLDS // world_size, args, rank, world_size, dev, distributed,
+                                f"BASELINE config 4: {CONFIG4_WORLDS} worlds sharded over {world_size} GPU(s) "
+                                "(strong scaling), step + shift + action write")
+            config4["scaling"] = "strong"
+            config4["total_worlds"] = CONFIG4_WORLDS
         secondary = reference_loop(4096, args, rank, world_size, dev, distributed,
                                    "BASELINE config 2: random-action rollout, obs/reward tensors "
                                    "on device (learn/training_loop.py call sequence)")
@@ -668,6 +678,8 @@ def main():
             out["config5"] = cfg5
         if config2:
             out["config2"] = config2
+        if config4:
+            out["config4"] = config4
         if secondary:
             out["secondary"] = secondary
             out["reference_loop"] = ref_main

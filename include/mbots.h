@@ -8,6 +8,8 @@
  * Plain pointers, sizes and status codes only (no torch / HIP C++ types).
  * Every function returns MBOTS_OK (0) or a negative MBOTS_E* code; the text of
  * the last error on the calling thread is available from mbots_last_error().
+ * The one positive status is mbots_step's MBOTS_W_CAPACITY (a warning: the
+ * step ran).
  * Streams are passed as `void *` holding a hipStream_t (NULL = default stream;
  * ignored in MBOTS_EXEC_CPU mode, where every call completes before returning).
  *
@@ -30,6 +32,16 @@ extern "C" {
 #define MBOTS_E_HIP        (-2)   /* HIP runtime error                  */
 #define MBOTS_E_NOMEM      (-3)   /* device / host allocation failed    */
 #define MBOTS_E_RANGE      (-4)   /* index out of range                 */
+#define MBOTS_E_CAPACITY   (-5)   /* mbots_step with MBOTS_FLAG_STRICT_CAPACITY:
+                                     agents were dropped at agent_capacity (the
+                                     step ran; see MBOTS_W_CAPACITY) */
+/* mbots_step warning (the step ran): since the last report, births or
+ * respawns were dropped because a world had reached agent_capacity.  The
+ * reference's tables have no cap (makeAgent in healthSync and in the respawn,
+ * sim.cpp:561-564, :830-834), so from that step on the run diverges from the
+ * reference's.  Reported from the row counts the device last published, so
+ * it can come a few steps after the drop (once per rise of mbots_overflow). */
+#define MBOTS_W_CAPACITY     1
 
 /* Manager::Config flags (build extensions; default 0 = reference-faithful) */
 #define MBOTS_FLAG_REWARD_FIXED     0x1u  /* rewards[speciesID-1] (fixes sim.cpp:943) */
@@ -44,6 +56,15 @@ extern "C" {
  * the views leaves them to replay their last actions (carried through the row
  * moves and the shift like every row's).  Every shard but the last sets it. */
 #define MBOTS_FLAG_SHARD_GHOST      0x4u
+/* a capacity drop (MBOTS_W_CAPACITY) is an error: mbots_step returns
+ * MBOTS_E_CAPACITY instead */
+#define MBOTS_FLAG_STRICT_CAPACITY  0x8u
+
+/* agent_capacity: 4..256 slots per world (MBOTS_MAX_CAPACITY).  The sensor's
+ * per-pixel depth key carries the object order (64 + slot for agents) in its
+ * low 9 bits, which bounds a world at 448 agents; the two built classes are
+ * 128 (default) and 256 slots. */
+#define MBOTS_MAX_CAPACITY          256u
 
 /* execution modes (madrona::ExecMode; the reference's callers pick CPU when
  * no GPU is present, learn/env.py:12-15) */
@@ -134,8 +155,12 @@ int mbots_num_agents(mbots_handle *h, uint32_t *out);
 int mbots_export(mbots_handle *h, int32_t export_id, mbots_tensor *out);
 /* Stream-ordered form (what the Python surface uses): any deferred copy or
  * join the view needs is enqueued on `stream`, after everything the manager
- * enqueued on the stream of its previous call, so the view is final in
- * stream order on `stream` (no host synchronisation). */
+ * enqueued on the stream of its previous call, so the view's data is final in
+ * stream order on `stream`.  The view's row count (dims[0] = N) is host
+ * state: the first call after a step waits once on the host for that step's
+ * row counts (mbots_num_agents); the data copies and joins themselves do not
+ * synchronise the host.  MBOTS_EXPORT_SENSOR_INDEX is computed on `stream`
+ * and synchronised before returning. */
 int mbots_export_on(mbots_handle *h, int32_t export_id, void *stream, mbots_tensor *out);
 /* Manager::setAction (mgr.cpp:251-272): row = export row (species-major). */
 int mbots_set_action(mbots_handle *h, uint32_t row, const int32_t action[6]);
@@ -273,6 +298,24 @@ int mbots_kernel_times(mbots_handle *h, double ms[MBOTS_TK_COUNT],
                        uint64_t launches[MBOTS_TK_COUNT]);
 
 const char *mbots_last_error(void);
+
+/* Environment.
+ * MBOTS_VALUE_FORK=0: the step's cross-stream hops (K1 -> the sensor's
+ *   internal stream, and the sensor back to the next step) are event waits.
+ *   Otherwise, at <= 8192 worlds and while the host runs ahead of the device,
+ *   they are hipStreamWaitValue32 waits on signal words a kernel stores (about
+ *   3 us instead of 7 per hop).  The runtime carries such a wait as a polling
+ *   kernel on the waiting stream; a tool or mode that runs the device's
+ *   kernels one at a time can dispatch that poller before its producer and
+ *   never finish it, so the value waits are also off whenever one of
+ *   MBOTS_SERIALISING_ENV is set (non-empty, not "0") when the manager is
+ *   created: rocprofv3 counter collection, an HSA tools library, a legacy
+ *   rocprof input file, or serialised kernel dispatch.
+ * MBOTS_CPU_THREADS: host threads of MBOTS_EXEC_CPU (default: the machine's
+ *   hardware threads, at most 16). */
+#define MBOTS_SERIALISING_ENV \
+    { "ROCPROF_COUNTER_COLLECTION", "HSA_TOOLS_LIB", "ROCP_INPUT", "AMD_SERIALIZE_KERNEL", \
+      "AMD_SERIALIZE_COPY" }
 
 #ifdef __cplusplus
 }

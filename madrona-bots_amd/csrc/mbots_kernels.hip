@@ -582,7 +582,12 @@ __device__ void world_step(SimState &S, const ObsTable &cur, WorldLDS<kCap> &L, 
         S.n_out[w] = nn;
         S.ctr[w] = ctr;
         S.cur_food[w] = cur_food;
-        if (ovf) S.overflow[w] += ovf;
+        if (ovf) {
+            S.overflow[w] += ovf;
+            // the running total the host checks after each step (MBOTS_W_CAPACITY);
+            // a shard ghost's drops belong to the next shard
+            if (w < S.Wx) atomicAdd(&S.totals[kTotOverflow], ovf);
+        }
     }
 }
 
@@ -713,6 +718,8 @@ __global__ __launch_bounds__(1024) void scan_kernel(SimState S, int parity)
                 __hip_atomic_store(S.totals_host + k, k ? (uint32_t)s_tot[k - 1] : (uint32_t)s_tot[4],
                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             __hip_atomic_store(S.totals_host + kTotRows, rows, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(S.totals_host + kTotOverflow, S.totals[kTotOverflow], __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
             // make the mirror visible before the dispatch's completion signal,
             // whatever scope the runtime gives that signal's release
             __threadfence_system();

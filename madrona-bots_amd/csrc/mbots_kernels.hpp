@@ -33,7 +33,7 @@ struct SimState {
     int32_t *src_of;                // [W*cap] new export row -> old row (-1: new agent)
     uint32_t *overflow;             // [W] dropped births/respawns
     uint32_t *totals;               // [0] = N, [1..4] = per-species rows, [kTotRows] = table rows
-                                    // incl. the shard ghost's (after row N)
+                                    // incl. the shard ghost's (after row N), [kTotOverflow]
     uint32_t *totals_host;          // mapped pinned mirror of totals (written by K2)
     int32_t *tiles;                 // [2][5][ntiles][kTileBuckets] per-tile species/agent counts (K1 -> K2)
     unsigned long long *agent_steps;
@@ -76,6 +76,8 @@ struct ObsTable {
 };
 
 constexpr int kTotRows = 5;   // totals[kTotRows]: rows the moves / shift / checkpoints cover
+constexpr int kTotOverflow = 6;   // totals[kTotOverflow]: births / respawns dropped at the
+                                  // capacity cap so far (exported worlds; K1 adds, K2 mirrors)
 uint32_t scan_tiles(uint32_t W);
 // whether the sensor renders worlds in K2's population order (every scan tile
 // full)

@@ -84,6 +84,9 @@ struct mbots_handle {
     unsigned long long join_capture = 0;   // stream-capture id it was recorded in (0: none)
     unsigned long long cap_seen = 0;  // the stream capture the last captured step belonged to
     uint64_t cap_steps = 0;           // steps recorded into it (mbots_join wants an even count)
+    bool poisoned = false;            // a graph of an odd number of steps was captured: the
+                                      // host's table bookkeeping no longer follows the device
+    uint32_t ovf_reported = 0;        // capacity drops reported so far (MBOTS_W_CAPACITY)
     // deferred K4 parts of a table half (moved from the other half along the
     // last src_of when needed): PrevAction / PrevHiddenState, the six other
     // Prev* columns (from the other half's current ones when six_lazy)
@@ -151,12 +154,15 @@ bool env_set(const char *name)
     const char *v = std::getenv(name);
     return v && *v && std::strcmp(v, "0") != 0;
 }
+// (the list and the switch are documented in include/mbots.h, "Environment")
 bool value_waits_safe()
 {
     const char *o = std::getenv("MBOTS_VALUE_FORK");
     if (o && std::strcmp(o, "0") == 0) return false;
-    return !(env_set("ROCPROF_COUNTER_COLLECTION") || env_set("AMD_SERIALIZE_KERNEL") ||
-             env_set("HSA_TOOLS_LIB") || env_set("ROCP_INPUT"));
+    static const char *const kSerialising[] = MBOTS_SERIALISING_ENV;
+    for (const char *name : kSerialising)
+        if (env_set(name)) return false;
+    return true;
 }
 bool fork_by_value(uint32_t W) { return W <= MB_VALUE_FORK_MAX && value_waits_safe(); }
 bool join_by_value(uint32_t W) { return MB_VALUE_JOIN && W <= MB_VALUE_JOIN_MAX && value_waits_safe(); }
@@ -291,6 +297,24 @@ bool capturing(hipStream_t st)
     return hipStreamIsCapturing(st, &cs) == hipSuccess && cs == hipStreamCaptureStatusActive;
 }
 
+// A graph captured with an odd number of steps leaves the table halves and the
+// host's deferred-move bookkeeping out of step with the device after a replay
+// (ADVICE r3/r4): every device entry point refuses to run from then on --
+// checked here (use_stream, sync_totals and the entry points that use neither)
+// and by mbots_step when the next capture starts.
+int capture_guard(mbots_handle *h, hipStream_t st)
+{
+    static const char *kMsg = "the last graph capture recorded an odd number of steps, so the manager's "
+                              "table halves no longer follow the device; capture an even number of steps "
+                              "(ending with join()) and create a new manager";
+    if (h->poisoned) return fail(MBOTS_E_INVALID, kMsg);
+    if ((h->cap_steps & 1) && !capturing(st)) {
+        h->poisoned = true;
+        return fail(MBOTS_E_INVALID, kMsg);
+    }
+    return MBOTS_OK;
+}
+
 // Every call enqueues on the caller's stream (torch's current stream); a call
 // on another stream than the previous one is ordered after everything the
 // manager enqueued there (an event hop), so steps, deferred copies and the
@@ -299,6 +323,7 @@ bool capturing(hipStream_t st)
 // cannot wait for work outside it.)
 int use_stream(mbots_handle *h, hipStream_t st)
 {
+    if (int rc = capture_guard(h, st)) return rc;
     if (st != h->last_stream && !capturing(st) && !capturing(h->last_stream)) {
         HIP_TRY(hipEventRecord(h->ev_hop, h->last_stream));
         HIP_TRY(hipStreamWaitEvent(st, h->ev_hop, 0));
@@ -432,6 +457,7 @@ int sync_totals(mbots_handle *h)
     // same step skip the runtime calls (the reference loop reads ~10 views per
     // step and is host-bound at small world counts, scripts/refhost.py) -- not
     // once graphs exist, whose replays change the counts behind the host's back
+    if (int rc = capture_guard(h, h->last_stream)) return rc;
     if (h->totals_ok && h->cap_seen == 0) return MBOTS_OK;
     HIP_TRY(hipSetDevice(h->device));
     // a host-side row count during stream capture would be the capture-time
@@ -607,6 +633,7 @@ int mbots_create(const mbots_config *cfg_in, mbots_handle **out)
     if (cfg.num_worlds == 0) return fail(MBOTS_E_INVALID, "num_worlds must be > 0");
     if (cfg.sensor_size != (uint32_t)mbots::kSensor)
         return fail(MBOTS_E_INVALID, "sensor_size must be 32 (mgr.hpp:19, entry.cpp:27)");
+    static_assert(mbots::kMaxCap == (int)MBOTS_MAX_CAPACITY, "include/mbots.h");
     if (cfg.agent_capacity > (uint32_t)mbots::kMaxCap || cfg.agent_capacity < 4)
         return fail(MBOTS_E_INVALID, "agent_capacity must be in [4, 256]");
     if (cfg.init_num_agents_per_world > cfg.agent_capacity)
@@ -750,12 +777,27 @@ int mbots_destroy(mbots_handle *h)
     return MBOTS_OK;
 }
 
+// MBOTS_W_CAPACITY / MBOTS_E_CAPACITY once per rise of the dropped-agent total
+static int capacity_report(mbots_handle *h, uint32_t dropped)
+{
+    if (dropped <= h->ovf_reported) return MBOTS_OK;
+    const uint32_t was = h->ovf_reported;
+    h->ovf_reported = dropped;
+    g_err = std::to_string(dropped - was) + " births / respawns dropped at agent_capacity " +
+            std::to_string(h->cfg.agent_capacity) + " (" + std::to_string(dropped) +
+            " in total): the reference's worlds have no cap (sim.cpp:561-564, :830-834), so the run now "
+            "differs from the reference's" +
+            (h->cfg.agent_capacity < MBOTS_MAX_CAPACITY ? std::string("; raise agent_capacity (at most 256)")
+                                                        : std::string(" (256 is the largest agent_capacity)"));
+    return (h->cfg.flags & MBOTS_FLAG_STRICT_CAPACITY) ? MBOTS_E_CAPACITY : MBOTS_W_CAPACITY;
+}
+
 int mbots_step(mbots_handle *h, void *stream)
 {
     if (!h) return fail(MBOTS_E_INVALID, "null handle");
     if (h->cpu) {
         h->cpu->step();
-        return MBOTS_OK;
+        return capacity_report(h, (uint32_t)std::min<uint64_t>(h->cpu->overflow(), 0xFFFFFFFFu));
     }
     HIP_TRY(hipSetDevice(h->device));
     hipStream_t st = as_stream(stream);
@@ -764,19 +806,14 @@ int mbots_step(mbots_handle *h, void *stream)
     unsigned long long cap_id = 0;
     HIP_TRY(hipStreamGetCaptureInfo(st, &cap_status, &cap_id));
     const bool capturing = cap_status == hipStreamCaptureStatusActive;
-    if (capturing) {
-        if (cap_id != h->cap_seen) { h->cap_seen = cap_id; h->cap_steps = 0; }
-        ++h->cap_steps;
-    } else if (h->cap_steps & 1) {
-        // a graph that ended without mbots_join holds an odd number of steps:
-        // every replay would leave the table halves and this bookkeeping out of
-        // step with the device
+    if (capturing && cap_id != h->cap_seen) {
+        // a new capture: the previous one must have held an even number of steps
+        if ((rc = capture_guard(h, nullptr))) return rc;
+        h->cap_seen = cap_id;
         h->cap_steps = 0;
-        return fail(MBOTS_E_INVALID, "the last graph capture recorded an odd number of steps; "
-                                     "capture an even number (and end it with join())");
     }
     if ((rc = use_stream(h, st))) return rc;
-    h->totals_ok = false;
+    if (capturing) ++h->cap_steps;
     const mbots::ObsTable &nxt = h->T[h->tb ^ 1];
     const int par = h->parity;
     const int lazy = h->prev_lazy[h->tb] ? 1 : 0;
@@ -831,6 +868,9 @@ int mbots_step(mbots_handle *h, void *stream)
         epoch = h->epoch;
     }
     h->S.epoch = h->sig_fork ? epoch : 0u;
+    // this step's row counts are K2's: no host read of them before it (ADVICE r4:
+    // cleared here, after every materialisation above that may sync the last ones)
+    h->totals_ok = false;
     rc = timed(h, MBOTS_TK_SCAN, st, [&] { return mbots::launch_scan(h->S, par, st, h->ev_totals, capturing); });
     h->S.epoch = 0;
     if (rc) return rc;
@@ -876,7 +916,9 @@ int mbots_step(mbots_handle *h, void *stream)
     if (prefetch & mbots::kMoveSensor) h->psem_pending[nt] = false;
     if (prefetch & mbots::kMovePrevAH) h->ah_pending[nt] = false;
     if (prefetch & mbots::kMovePrev6) h->six_pending[nt] = false;
-    return MBOTS_OK;
+    // capacity drops the device has published so far (K2's pinned mirror of a
+    // recent step: no synchronisation)
+    return capacity_report(h, __atomic_load_n(&h->h_totals[mbots::kTotOverflow], __ATOMIC_RELAXED));
 }
 
 int mbots_shift_observations(mbots_handle *h, void *stream)
@@ -1369,6 +1411,7 @@ int mbots_save_checkpoint(mbots_handle *h, void *dst, uint64_t bytes)
         return r ? fail(r, err) : MBOTS_OK;
     }
     HIP_TRY(hipSetDevice(h->device));
+    if (int rc = capture_guard(h, h->last_stream)) return rc;
     int rc0 = materialize_prev(h, h->last_stream);
     if (!rc0) rc0 = materialize_prev_ah(h, h->last_stream);
     if (!rc0) rc0 = materialize_cur_ah(h, h->last_stream, 3);
@@ -1408,7 +1451,9 @@ int mbots_load_checkpoint(mbots_handle *h, const void *src, uint64_t bytes)
     if (h->cpu) {
         std::string err;
         const int r = h->cpu->load(src, bytes, err);
-        return r ? fail(r, err) : MBOTS_OK;
+        if (r) return fail(r, err);
+        h->ovf_reported = (uint32_t)std::min<uint64_t>(h->cpu->overflow(), 0xFFFFFFFFu);
+        return MBOTS_OK;
     }
     if (bytes < sizeof(CkptHeader)) return fail(MBOTS_E_INVALID, "checkpoint truncated");
     CkptHeader hd;
@@ -1421,11 +1466,27 @@ int mbots_load_checkpoint(mbots_handle *h, const void *src, uint64_t bytes)
         return fail(MBOTS_E_INVALID, "checkpoint configuration differs from the manager's");
     if (hd.n_rows > (uint64_t)h->S.W * h->cfg.agent_capacity)
         return fail(MBOTS_E_INVALID, "checkpoint row count out of range");
-    HIP_TRY(hipSetDevice(h->device));
-    HIP_TRY(hipDeviceSynchronize());
+    if (int rc = capture_guard(h, h->last_stream)) return rc;
     const auto segs = ckpt_segments(h, h->T[0], hd.n_rows);
     if (bytes < ckpt_bytes(segs) || hd.bytes != ckpt_bytes(segs))
         return fail(MBOTS_E_INVALID, "checkpoint size mismatch");
+    {
+        // the blob's own totals must agree with its header before anything is
+        // overwritten (a mismatch used to leave the manager half restored)
+        const char *q = static_cast<const char *>(src) + sizeof(hd);
+        for (const Seg &s : segs) {
+            if (s.p == h->S.totals) {
+                uint32_t tot[8];
+                memcpy(tot, q, sizeof(tot));
+                if (tot[mbots::kTotRows] != hd.n_rows || tot[0] > hd.n_rows)
+                    return fail(MBOTS_E_INVALID, "checkpoint row count disagrees with its saved totals");
+                break;
+            }
+            q += s.bytes;
+        }
+    }
+    HIP_TRY(hipSetDevice(h->device));
+    HIP_TRY(hipDeviceSynchronize());
     const char *p = static_cast<const char *>(src) + sizeof(hd);
     for (const Seg &s : segs) {
         if (s.bytes) HIP_TRY(hipMemcpy(s.p, p, s.bytes, hipMemcpyHostToDevice));
@@ -1451,8 +1512,7 @@ int mbots_load_checkpoint(mbots_handle *h, const void *src, uint64_t bytes)
     int rc = record_totals(h, st);
     if (rc) return rc;
     HIP_TRY(hipDeviceSynchronize());
-    if (h->h_totals[mbots::kTotRows] != hd.n_rows)
-        return fail(MBOTS_E_INVALID, "checkpoint row count disagrees with its saved totals");
+    h->ovf_reported = h->h_totals[mbots::kTotOverflow];   // drops before the checkpoint were reported then
     return MBOTS_OK;
 }
 

@@ -21,14 +21,15 @@ without a GPU raises RuntimeError (no silent fallback).
 import ctypes
 import os
 import types
+import warnings
 
 import torch  # loads the HIP runtime libmbots.so links against (same soname)
 
-__all__ = ["SimManager", "Tensor", "madrona", "ExportID", "ExecMode", "unpack_rollout", "unpack_learner"]
+__all__ = ["SimManager", "Tensor", "madrona", "ExportID", "ExecMode", "unpack_rollout", "unpack_learner",
+           "CapacityWarning", "CapacityError", "MAX_CAPACITY"]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-# MBOTS_LIB: developer override to A/B alternative builds of the same library
-_LIB_PATH = os.environ.get("MBOTS_LIB") or os.path.join(_HERE, "libmbots.so")
+_LIB_PATH = os.path.join(_HERE, "libmbots.so")
 
 if not os.path.exists(_LIB_PATH):
     raise ImportError(
@@ -90,11 +91,7 @@ def _load():
         "mbots_kernel_times": [vp, P(ctypes.c_double), P(ctypes.c_uint64)],
     }
     for name, args in sig.items():
-        # (a symbol an older build lacks -- A/B runs through MBOTS_LIB -- stays
-        # absent: calling it raises AttributeError)
-        fn = getattr(L, name, None)
-        if fn is None and os.environ.get("MBOTS_LIB"):
-            continue
+        fn = getattr(L, name)
         fn.argtypes = args
         fn.restype = ctypes.c_int
     L.mbots_last_error.restype = ctypes.c_char_p
@@ -108,7 +105,21 @@ _lib = _load()
 def _check(rc):
     if rc != 0:
         msg = _lib.mbots_last_error().decode(errors="replace")
-        raise RuntimeError(f"madrona_bots: {msg} (status {rc})")
+        raise (CapacityError if rc == _E_CAPACITY else RuntimeError)(f"madrona_bots: {msg} (status {rc})")
+
+
+_W_CAPACITY, _E_CAPACITY = 1, -5   # include/mbots.h MBOTS_W_CAPACITY / MBOTS_E_CAPACITY
+MAX_CAPACITY = 256                 # MBOTS_MAX_CAPACITY
+
+
+class CapacityWarning(RuntimeWarning):
+    """Births or respawns were dropped because a world reached agent_capacity:
+    the reference's worlds have no cap (sim.cpp:561-564, :830-834), so the run
+    now differs from the reference's (MBOTS_W_CAPACITY)."""
+
+
+class CapacityError(RuntimeError):
+    """CapacityWarning under strict_capacity=True (MBOTS_E_CAPACITY); the step ran."""
 
 
 class ExportID:
@@ -132,6 +143,7 @@ def _raw_stream(device):
 FLAG_REWARD_FIXED = 0x1
 FLAG_FIX_DEPTH_ALIAS = 0x2
 FLAG_SHARD_GHOST = 0x4
+FLAG_STRICT_CAPACITY = 0x8
 
 
 class ExecMode:
@@ -157,11 +169,32 @@ OBS_DIM = 69   # learn/env.py:19
 KERNELS = ("world_step", "scan", "export", "sensor", "shift", "actions", "move", "obs")
 
 
+class _Handle:
+    """One manager's library handle (mbots_create / mbots_destroy).  Every
+    exported view holds it -- a torch view's storage holds the Tensor whose
+    array interface it was built from, and that Tensor holds this -- so a view
+    outlives the SimManager that produced it.  The manager's view
+    cache holds views, which hold this handle and never the manager, so there
+    is no reference cycle: the device memory is freed by reference counting
+    once the manager and every view of it are gone."""
+    __slots__ = ("h",)
+
+    def __init__(self, h):
+        self.h = h
+
+    def __del__(self):
+        h = self.h
+        if h and _lib is not None:   # module globals may be gone at interpreter exit
+            _lib.mbots_destroy(h)
+            self.h = None
+
+
 class Tensor:
     """Non-owning device tensor view (madrona::py::Tensor)."""
 
-    def __init__(self, owner, ct, column=False):
-        self._owner = owner          # keeps the manager (and its memory) alive
+    def __init__(self, keep, ct, column=False, mgr=None):
+        self._keep = keep            # the manager's _Handle: keeps its memory alive
+        self._mgr = mgr              # the manager (its view cache), for table columns
         self._column = column        # a table column: W x cap row slots behind it
         self._ptr = int(ct.data or 0)
         self._torch_dtype, self._typestr = _DTYPES[ct.dtype]
@@ -191,7 +224,7 @@ class Tensor:
         # the learner reads ~10 views per step and is host-bound at small world
         # counts (scripts/refhost.py); building a view from the array interface
         # every time is most of an accessor's host cost
-        base = self._owner._view_cache(self) if self._column else None
+        base = self._mgr._view_cache(self) if (self._column and self._mgr is not None) else None
         if base is not None:
             return base[:self.shape[0]]
         t = torch.as_tensor(self, device=dev)
@@ -207,6 +240,7 @@ class Tensor:
         if n == 0:
             return torch.empty(self.shape, dtype=self._torch_dtype)
         buf = (ctypes.c_char * (n * np.dtype(npdt).itemsize)).from_address(self._ptr)
+        buf._keep = self._keep       # the view (numpy base -> buffer) keeps the manager's memory
         t = torch.from_numpy(np.frombuffer(buf, dtype=npdt, count=n).reshape(self.shape))
         if t.data_ptr() != self._ptr:
             raise RuntimeError("madrona_bots: to_torch() produced a copy, expected a view")
@@ -283,33 +317,32 @@ class SimManager:
     off-by-one), fix_depth_alias (depth_tensor returns real depth,
     SURVEY B.1), shard_ghost (also step world world_offset + num_worlds, never
     exported, so a shard's faithful B.3 rewards equal one device's; its agents
-    act on the write_synthetic_actions stream)."""
+    act on the write_synthetic_actions stream), strict_capacity (a world that
+    reaches agent_capacity -- at most MAX_CAPACITY = 256 slots -- and drops a
+    birth or respawn makes step() raise CapacityError instead of warning with
+    CapacityWarning: the reference has no cap)."""
 
     def __init__(self, gpu_id, num_worlds, rand_seed, init_num_agents_per_world, *,
                  exec_mode="hip", agent_capacity=128, world_offset=0, reward_fixed=False,
-                 fix_depth_alias=False, shard_ghost=False):
+                 fix_depth_alias=False, shard_ghost=False, strict_capacity=False):
         self.exec_mode = _exec_mode(exec_mode)
         self.gpu_id = int(gpu_id)
         self.num_worlds = int(num_worlds)
         self.agent_capacity = int(agent_capacity)
         flags = (FLAG_REWARD_FIXED if reward_fixed else 0) | \
                 (FLAG_FIX_DEPTH_ALIAS if fix_depth_alias else 0) | \
-                (FLAG_SHARD_GHOST if shard_ghost else 0)
+                (FLAG_SHARD_GHOST if shard_ghost else 0) | \
+                (FLAG_STRICT_CAPACITY if strict_capacity else 0)
         cfg = _Config(self.gpu_id, self.num_worlds, int(rand_seed) & 0xFFFFFFFF,
                       int(init_num_agents_per_world), 32, int(world_offset),
                       int(agent_capacity), flags, self.exec_mode)
         h = ctypes.c_void_p()
         _check(_lib.mbots_create(ctypes.byref(cfg), ctypes.byref(h)))
+        self._hd = _Handle(h)        # destroyed when the manager and all its views are gone
         self._h = h
         # row slots of every table column (the shard ghost is one more world)
         self._cap_rows = (self.num_worlds + (1 if shard_ghost else 0)) * self.agent_capacity
         self._views = {}
-
-    def __del__(self):
-        h = getattr(self, "_h", None)
-        if h and _lib is not None:   # module globals may be gone at interpreter exit
-            _lib.mbots_destroy(h)
-            self._h = None
 
     def _stream(self):
         if self.exec_mode == ExecMode.CPU:
@@ -327,8 +360,9 @@ class SimManager:
         key = (tensor._ptr, tensor._torch_dtype, cols)
         base = self._views.get(key)
         if base is None:
-            full = Tensor(None, _CTensor(tensor._ptr, _DTYPE_CODE[tensor._torch_dtype], tensor._device,
-                                         (ctypes.c_int64 * 2)(cap_rows, cols)))
+            # (owned by the handle, not the manager: no cycle through the cache)
+            full = Tensor(self._hd, _CTensor(tensor._ptr, _DTYPE_CODE[tensor._torch_dtype], tensor._device,
+                                             (ctypes.c_int64 * 2)(cap_rows, cols)))
             base = torch.as_tensor(full, device=torch.device("cuda", tensor._device))
             if base.data_ptr() != tensor._ptr:
                 raise RuntimeError("madrona_bots: to_torch() produced a copy, expected a view")
@@ -344,7 +378,12 @@ class SimManager:
 
     # -- graphs -------------------------------------------------------------
     def step(self):
-        _check(_lib.mbots_step(self._h, self._stream()))
+        rc = _lib.mbots_step(self._h, self._stream())
+        if rc == _W_CAPACITY:   # the step ran; agents were dropped at the cap (reported late by a few steps)
+            warnings.warn(f"madrona_bots: {_lib.mbots_last_error().decode(errors='replace')}",
+                          CapacityWarning, stacklevel=2)
+        elif rc:
+            _check(rc)
 
     def shift_observations(self):
         _check(_lib.mbots_shift_observations(self._h, self._stream()))
@@ -355,11 +394,8 @@ class SimManager:
         # and joins are enqueued there, after everything the manager enqueued
         # on whatever stream its previous call used (mbots_export_on)
         ct = _CTensor()
-        if getattr(_lib, "mbots_export_on", None) is None:   # an older build under MBOTS_LIB (A/B)
-            _check(_lib.mbots_export(self._h, eid, ctypes.byref(ct)))
-        else:
-            _check(_lib.mbots_export_on(self._h, eid, self._stream(), ctypes.byref(ct)))
-        return Tensor(self, ct, column=eid not in (ExportID.SpeciesCount, ExportID.Reset))
+        _check(_lib.mbots_export_on(self._h, eid, self._stream(), ctypes.byref(ct)))
+        return Tensor(self._hd, ct, column=eid not in (ExportID.SpeciesCount, ExportID.Reset), mgr=self)
 
     def depth_tensor(self, is_prev=False):
         return self._export(ExportID.PrevSensorDepth if is_prev else ExportID.SensorDepth)

@@ -7,6 +7,6 @@ n=${1:-2}; shift
 for r in $(seq $n); do
   timeout -k 10 120 python scripts/kbench.py --no-kernel-timing "$@" || exit 1
   for lib in build_var/libmbots_*.so; do
-    MBOTS_LIB=$lib timeout -k 10 120 python scripts/kbench.py --no-kernel-timing "$@" || exit 1
+    MBOTS_LIB=$lib timeout -k 10 120 python scripts/run_variant.py scripts/kbench.py --no-kernel-timing "$@" || exit 1
   done
 done

@@ -8,6 +8,6 @@ libs=(); while [ $# -gt 0 ] && [ "$1" != "--" ]; do libs+=("$1"); shift; done
 [ "$1" = "--" ] && shift
 for r in $(seq 1 $rounds); do
   for lib in "${libs[@]}"; do
-    MBOTS_LIB=$lib timeout -k 10 120 python scripts/kbench.py --no-kernel-timing "$@" || exit 1
+    MBOTS_LIB=$lib timeout -k 10 120 python scripts/run_variant.py scripts/kbench.py --no-kernel-timing "$@" || exit 1
   done
 done

@@ -6,6 +6,8 @@ the device sets the pace (a device-bound loop lets the host run ahead).
 import argparse, json, os, sys, time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "madrona-bots_amd"))
+sys.path.insert(0, os.path.join(ROOT, "scripts"))
+import _variant  # noqa: E402,F401  (MBOTS_LIB: A/B builds)
 import torch
 import madrona_bots as mb
 

@@ -7,7 +7,7 @@ mkdir -p gpurun_out
 : > gpurun_out/bench_ab.log
 for r in $(seq ${ROUNDS:-3}); do
   for l in build_var/libmbots_*.so; do
-    MBOTS_LIB=$l timeout -k 10 180 python bench.py --no-cpu-baseline --no-secondary --no-kernel-timing \
+    MBOTS_LIB=$l timeout -k 10 180 python scripts/run_variant.py bench.py --no-cpu-baseline --no-secondary --no-kernel-timing \
         --steps ${STEPS:-200} ${BENCH_ARGS:-} 2>/dev/null | grep '^{' | \
         python -c "import sys, json; d = json.loads(sys.stdin.read()); print(json.dumps({'lib': '$l', 'ms': d['ms_per_step']}))" \
         >> gpurun_out/bench_ab.log || exit 1

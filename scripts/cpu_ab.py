@@ -3,7 +3,7 @@
 counts, interleaved: python scripts/cpu_ab.py lib1.so lib2.so ... """
 import os, subprocess, sys, json
 code = r'''
-import sys, time, os; sys.path.insert(0, "madrona-bots_amd")
+import sys, time, os; sys.path.insert(0, "madrona-bots_amd"); sys.path.insert(0, "scripts"); import _variant
 import madrona_bots as mb
 W = int(os.environ["W"])
 s = mb.SimManager(0, W, 69, 32, exec_mode="cpu")

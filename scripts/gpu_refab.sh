@@ -9,7 +9,7 @@ mkdir -p gpurun_out
 for r in $(seq ${ROUNDS:-3}); do
   for l in build_var/libmbots_*.so; do
     for wv in ${WORLDS:-4096 65536}; do
-      MBOTS_LIB=$l timeout -k 10 120 python scripts/refloop.py --worlds $wv --steps ${STEPS:-200} \
+      MBOTS_LIB=$l timeout -k 10 120 python scripts/run_variant.py scripts/refloop.py --worlds $wv --steps ${STEPS:-200} \
           >> gpurun_out/refab.log 2>&1 || { tail -5 gpurun_out/refab.log; exit 1; }
     done
   done

@@ -11,6 +11,8 @@ so this is a latency measurement, not a bench line.
 import argparse, json, os, sys, time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "madrona-bots_amd"))
+sys.path.insert(0, os.path.join(ROOT, "scripts"))
+import _variant  # noqa: E402,F401  (MBOTS_LIB: A/B builds)
 import torch
 import madrona_bots as mb
 

@@ -4,7 +4,7 @@ counter into the overflow column): counter total / (worlds x steps)."""
 import glob, os, subprocess, sys, json
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 code = r'''
-import sys, json; sys.path.insert(0, "madrona-bots_amd")
+import sys, json; sys.path.insert(0, "madrona-bots_amd"); sys.path.insert(0, "scripts"); import _variant
 import torch, madrona_bots as mb
 W = 65536
 m = mb.SimManager(0, W, 69, 32)

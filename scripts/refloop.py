@@ -5,6 +5,8 @@ import argparse, json, os, sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "madrona-bots_amd"))
+sys.path.insert(0, os.path.join(ROOT, "scripts"))
+import _variant  # noqa: E402,F401  (MBOTS_LIB: A/B builds)
 import torch
 import bench
 

@@ -172,3 +172,26 @@ def test_checkpoint_load_then_save_before_stepping(ghost):
     c = mb.SimManager(0, 64, 5, 32, **kw)
     with pytest.raises(RuntimeError, match="version"):
         c.load_checkpoint(old)
+
+
+@pytest.mark.gpu
+def test_checkpoint_with_bad_totals_leaves_manager_intact():
+    """a blob whose saved row count disagrees with its header is
+    refused before anything is overwritten (the target keeps its own state)."""
+    import madrona_bots as mb
+    a = mb.SimManager(0, 64, 5, 32)
+    _run(a, 0, 5)
+    blob = a.save_checkpoint()
+    b = mb.SimManager(0, 64, 5, 32)
+    _run(b, 0, 2)
+    mine = b.save_checkpoint()
+    # header (48 B), 11 agent columns of 64 x 128 slots, the per-world arrays
+    # (n, ctr, key, food, food_rot, cur_food, sreward, scount, row_base,
+    # world_off, overflow: 1420 B per world), then totals[8]
+    tot = 48 + 11 * 64 * 128 * 4 + 64 * 1420
+    assert int(np.frombuffer(blob[tot + 20:tot + 24].tobytes(), np.uint32)[0]) == a.num_rows()
+    bad = blob.copy()
+    bad[tot + 20:tot + 24] = np.frombuffer(np.uint32(a.num_rows() + 1).tobytes(), np.uint8)
+    with pytest.raises(RuntimeError, match="disagrees"):
+        b.load_checkpoint(bad)
+    assert np.array_equal(b.save_checkpoint(), mine)

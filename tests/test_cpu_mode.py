@@ -156,10 +156,17 @@ def _same(h, c, where):
 def test_breed_heavy_to_capacity_256():
     """A breed-heavy stream fills worlds to 256 slots; births past it are
     dropped and counted exactly as the oracle does."""
+    import madrona_bots as mb
     W = 16
     mgr = _mgr(W, agent_capacity=256)
     orc = pyoracle.OracleSim(W, 69, 32, cap=256, num_threads=4)
-    for t in range(40):
+    with pytest.warns(mb.CapacityWarning, match="256 is the largest"):
+        _breed_steps(mgr, orc, 40)
+    assert mgr.overflow() == orc.overflow() > 0
+
+
+def _breed_steps(mgr, orc, steps):
+    for t in range(steps):
         g = torch.Generator().manual_seed(1000 + t)
         n = mgr.num_agents()
         r = torch.randint(0, 8, (n,), generator=g)
@@ -176,7 +183,6 @@ def test_breed_heavy_to_capacity_256():
         assert not errs, errs[:5]
         mgr.shift_observations()
         orc.shift_observations()
-    assert mgr.overflow() == orc.overflow() > 0
 
 
 @pytest.mark.gpu

@@ -47,14 +47,17 @@ def _own_views(m):
 
 
 def _bitwise(a, b):
-    return a.shape == b.shape and torch.equal(a.contiguous().view(torch.int32).cpu(),
-                                              b.contiguous().view(torch.int32).cpu())
+    if a.device != b.device:
+        a, b = a.cpu(), b.cpu()
+    return a.shape == b.shape and torch.equal(a.contiguous().view(torch.int32), b.contiguous().view(torch.int32))
 
 
-def _roundtrip_in_process(shards, full, steps):
+def _roundtrip_in_process(shards, full, steps, full_records=False):
     """Shards and the full manager in one process: the gather / scatter data
     movement of harness/gather.py without the collectives (the reassembly and
-    its inverse are the same functions)."""
+    its inverse are the same functions).  full_records: the gathered tensors
+    are also compared with the full manager's own learner records
+    (pack_learner -> unpack_learner)."""
     sys.path.insert(0, HARNESS)
     import gather
     import madrona_bots as mb
@@ -71,7 +74,13 @@ def _roundtrip_in_process(shards, full, steps):
         got = mb.unpack_learner(recs)
         ref = _own_views(full)
         bad += [f"step {t}: {k}" for k in ref if not _bitwise(got[k], ref[k])]
+        if full_records:
+            own = mb.unpack_learner(full.pack_learner())
+            bad += [f"step {t}: {k} (records)" for k in own if not _bitwise(got[k], own[k])]
+            del own
+        del ref
         actions, memory = _learner(got, t)
+        del got
         for m in shards + [full]:
             m.shift_observations()
         full.write_actions(actions, memory)
@@ -221,3 +230,25 @@ def test_learner_roundtrip_over_rccl_one_rank():
     learner records, scatter of actions + memory) executed by RCCL on the
     device at one rank: equal to a manager driven through write_actions."""
     assert _spawn(_rccl_worker, 1) == []
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("fix_depth", [False, True])
+def test_config5_eight_shards_at_full_size(fix_depth):
+    """BASELINE config 5 at its own size: 262144 worlds as
+    8 x 32768-world shards on one device (ranks 0..6 with their shard ghosts),
+    against one 262144-world manager, 3 steps of the learner round trip of
+    learn/training_loop.py:43-93, :136-137: every shard's pack_learner ->
+    reassemble -> unpack_learner == the full manager's views and its own
+    pack_learner -> unpack_learner, bitwise on every key; split_rows +
+    write_actions drive the 8 shards with the learner's actions and memory
+    exactly as write_actions drives the full manager.  (The RCCL transport
+    between 8 GPUs is the driver's multi-GPU run.)"""
+    import madrona_bots as mb
+    R, WS = 8, 32768
+    kw = dict(fix_depth_alias=fix_depth)
+    shards = [mb.SimManager(0, WS, SEED, 32, world_offset=r * WS, shard_ghost=r < R - 1, **kw) for r in range(R)]
+    full = mb.SimManager(0, R * WS, SEED, 32, **kw)
+    assert _roundtrip_in_process(shards, full, 3, full_records=True) == []
+    assert sum(m.num_agents() for m in shards) == full.num_agents() > 8 * WS * 30
