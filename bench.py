@@ -18,7 +18,12 @@ rank 0 picks actions and memory, and they are scattered back to the ranks that
 own the rows (madrona-bots_amd/harness/gather.py); reported as "config5".
 `python bench.py --gpus N` without a launcher starts the N ranks itself.
 
-After the main line (unless --no-secondary): the reference training loop's
+After the main line (unless --no-secondary): "steady_state", the same loop
+from step 250 on, once the worlds' food has reached its cap (the per-step cost
+rises with the food count over the first ~250 steps, so the early window of a
+short run is not the long-run rate: profiles/r05_drivergap.json); "config2",
+the same loop at 4096 worlds/GPU; "config4", BASELINE config 4's 262144 worlds
+sharded over the N ranks (strong scaling); and the reference training loop's
 call sequence (learn/training_loop.py:36-137 without the learner math: step,
 the action / memory views, reward and health clones, construct_obs of the
 current and previous rows, PrevHiddenState, shift, the learner's one-hot
@@ -49,6 +54,7 @@ SEED = 69                   # learn/env.py:15
 ACTION_SEED = 1234
 AGENTS_PER_WORLD = 32       # learn/env.py:15
 CONFIG4_WORLDS = 262144     # BASELINE config 4 (sharded across 8 GPUs)
+STEADY_FROM, STEADY_STEPS = 250, 100   # the steady-state line: food at its cap
 
 
 def algorithmic_bytes(n_agents, n_worlds):
@@ -535,6 +541,44 @@ def main():
         torch.cuda.synchronize()
         ktimes = mgr.kernel_times()
         mgr.enable_kernel_timing(False)
+        t = args.warmup + args.steps + min(args.steps, 50)
+    else:
+        t = args.warmup + args.steps
+    # the same loop once the worlds' food has reached its cap (30 per world,
+    # from about step 200 on; the first steps run with little food, so the
+    # sensor has fewer objects to test: profiles/r05_drivergap.json)
+    steady = None
+    if not args.no_secondary:
+        while t < STEADY_FROM:
+            one_step(t)
+            t += 1
+        torch.cuda.synchronize()
+        s0 = mgr.agent_steps()
+        if distributed:
+            dist.barrier()
+        torch.cuda.synchronize()
+        ts0 = time.perf_counter()
+        for k in range(STEADY_STEPS):
+            one_step(t + k)
+        torch.cuda.synchronize()
+        el_s = time.perf_counter() - ts0
+        n_s = mgr.agent_steps() - s0
+        st_s = torch.tensor([el_s, float(n_s)], dtype=torch.float64, device=dev if args.backend == "nccl" else "cpu")
+        tot_s = float(n_s)
+        if distributed:
+            dist.barrier()
+            tm_s = st_s[0:1].clone(); dist.all_reduce(tm_s, op=dist.ReduceOp.MAX)
+            tt_s = st_s[1:2].clone(); dist.all_reduce(tt_s, op=dist.ReduceOp.SUM)
+            el_s, tot_s = float(tm_s.item()), float(tt_s.item())
+        nb_s = algorithmic_bytes(n_s / STEADY_STEPS, W)
+        ms_s = el_s / STEADY_STEPS * 1e3
+        steady = {"what": f"the headline loop at steps {t}-{t + STEADY_STEPS - 1} (food at its cap of 30 per world)",
+                  "value": tot_s / el_s, "unit": "agent-steps/s", "ms_per_step": ms_s, "steps": STEADY_STEPS,
+                  "mean_agents_per_world": n_s / STEADY_STEPS / W,
+                  "roofline": {"bound": "hbm", "achieved": nb_s / (ms_s * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
+                               "unit": "GB/s", "frac": nb_s / (ms_s * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                               "algorithmic_bytes_per_step": nb_s,
+                               "timing": "wall clock of the timed steps (step + shift + action write)"}}
     # config 5 (BASELINE: sim + learner on rank 0, RCCL gather of the rollout
     # tensors): its own timed loop after the main line, by default whenever the
     # bench runs several ranks (so the driver's 1..8-GPU run covers it)
@@ -680,6 +724,8 @@ def main():
             out["config2"] = config2
         if config4:
             out["config4"] = config4
+        if steady:
+            out["steady_state"] = steady
         if secondary:
             out["secondary"] = secondary
             out["reference_loop"] = ref_main

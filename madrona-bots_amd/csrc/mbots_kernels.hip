@@ -195,8 +195,10 @@ __device__ __forceinline__ void init_slot(WorldLDS<kCap> &L, int s, float x, flo
 // SortArchetypeNode<Agent, WorldID> (sim.cpp:1061-1132).
 // ---------------------------------------------------------------------------
 template <int kCap>
-__device__ void world_step(SimState &S, const ObsTable &cur, WorldLDS<kCap> &L, uint32_t w,
-                           uint32_t lane);
+struct FinderScratch;
+template <int kCap, bool kFinder>
+__device__ void world_step(SimState &S, const ObsTable &cur, WorldLDS<kCap> &L, FinderScratch<kCap> &F,
+                           uint32_t w, uint32_t lane);
 
 #ifndef MB_K1_WPB
 #define MB_K1_WPB 8   // 4: K1 +2.5 %, and +7 % step at 4096 worlds; 16: +30 % K1
@@ -205,16 +207,20 @@ constexpr int kK1Worlds = MB_K1_WPB;          // worlds (waves) per K1 block
 // SGPRs capped at 80: the compiler's own choice (99, no spill at 80) admits only
 // 6 waves per SIMD (800 SGPRs per SIMD in 16-register granules plus 16), one
 // block in four fewer: K1 87 -> 78 us, step -1.7 %
-template <int kCap>
+// kFinder: the finder slots this step reads computed here (world_finders)
+// instead of read from the last step's sensor, so K1 need not wait for it
+// (small world counts, where the step is a latency chain)
+template <int kCap, bool kFinder>
 __global__ __launch_bounds__(64 * kK1Worlds, (kCap <= 128 ? 32 : 16) / kK1Worlds)
 __attribute__((amdgpu_num_sgpr(80))) void world_step_kernel(
     SimState S, ObsTable cur, int parity)
 {
     __shared__ WorldLDS<kCap> lds[kK1Worlds];
+    __shared__ FinderScratch<kCap> fsc[kFinder ? kK1Worlds : 1];
     const uint32_t wv = threadIdx.x >> 6;
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t w = uniform(blockIdx.x * kK1Worlds + wv);
-    if (w < S.W) world_step(S, cur, lds[wv], w, lane);
+    if (w < S.W) world_step<kCap, kFinder>(S, cur, lds[wv], fsc[kFinder ? wv : 0], w, lane);
     // counter-major tile buckets: [counter][tile][bucket] (K2 reads one
     // counter's buckets as contiguous 16-B words)
     const size_t nent = (size_t)S.ntiles * kTileBuckets;
@@ -245,9 +251,202 @@ __attribute__((amdgpu_num_sgpr(80))) void world_step_kernel(
     }
 }
 
+// ---------------------------------------------------------------------------
+// K1's finder pass (small world counts): the finder slots this step's actions
+// read -- what the last step's sensor computed for its centre ray
+// (sim.cpp:1183-1188, read by actionSystem / healthSync :434-454, :547-569;
+// the forward ray u = 0, the nearest object by (depth, order)
+// beyond the near sphere, an agent's slot if it beats the wall) -- evaluated
+// here on the world as K1 staged it (the state the sensor saw) with the
+// sensor's predicates (finder_key for discs, box_hit at u = 0 for food
+// squares, its wall resolution), so this K1 need not wait for that sensor.
+// Only the agents that shoot or breed read their slot: they are the cameras
+// (every slot past 64 too, whose action row is loaded later).  A P1-style cull
+// of every (camera, object) pair -- |l| <= 1.45 and f >= -0.35 are necessary
+// for either kind: a disc is hit only where |l| <= R and f >= 1.1 - R, a
+// square only where |l| <= |p| + |q| <= sqrt 2 and f + ext >= 1.1 -- then the
+// exact test of the survivors (about one per camera), atomicMin of their keys.
+// ---------------------------------------------------------------------------
+constexpr float kFinderCullL = 1.45f, kFinderCullF = -0.35f;
+
 template <int kCap>
-__device__ void world_step(SimState &S, const ObsTable &cur, WorldLDS<kCap> &L, uint32_t w,
-                           uint32_t lane)
+struct FinderScratch {
+    uint32_t queue[128];   // cull survivors: camera | object << 8 (flushed at >= 64)
+    uint8_t cam[kCap];     // the cameras' slots
+};
+
+template <int kCap>
+__device__ void world_finders(const SimState &S, WorldLDS<kCap> &L, FinderScratch<kCap> &F, uint32_t lane,
+                              int n0, uint64_t food_rec, const uint32_t (&rot)[kMaxPkg], bool want0)
+{
+    constexpr int kG = kCap / 64;
+    static_assert(kCap * 4 >= 2 * kMaxFood * 8, "food scratch in the take array");
+    // scratch: healthSync's arrays, free until it runs
+    uint32_t *const fkey = reinterpret_cast<uint32_t *>(L.key);   // [ncam] min key per camera
+    float2 *const fobj = reinterpret_cast<float2 *>(L.take);      // [na] food positions (NaN gap)
+    float2 *const frot = fobj + kMaxFood;                         // [nf] food (cos, sin)
+
+    // ---- cameras: the slots that shoot or breed (and every slot past 64) ----
+    int ncam = 0;
+#pragma unroll
+    for (int g = 0; g < kG; ++g) {
+        const int sl = 64 * g + (int)lane;
+        if (64 * g >= n0) break;
+        const bool want = sl < n0 && (g > 0 || want0);
+        const uint64_t m = ballot64(want);
+        if (want) F.cam[ncam + (int)rank_below(m)] = (uint8_t)sl;
+        ncam += __popcll(m);
+        if (sl < n0) L.finder[sl] = -1;
+    }
+    // ---- live food packages in (chunk, package) order (the sensor's objects) ----
+    const uint32_t live = lane < kNumChunks ? (uint32_t)(food_rec >> 40) & 31u : 0u;
+    const int cnt = __popc(live);
+    int off = 0, tot = 0;
+#pragma unroll
+    for (int bt = 0; bt < 3; ++bt) {
+        const uint64_t m = ballot64((cnt >> bt) & 1);
+        off += (int)rank_below(m) << bt;
+        tot += __popcll(m) << bt;
+    }
+    const int nf = min(tot, kMaxFood);
+    const int na = (nf + 7) & ~7;
+    {
+        const float bx = (float)((lane % kChunksX) * kChunkW), by = (float)((lane / kChunksX) * kChunkW);
+        int so = off;
+#pragma unroll
+        for (int k = 0; k < kMaxPkg; ++k) {
+            if ((live >> k) & 1u) {
+                const uint32_t xy = (uint32_t)(food_rec >> (8 * k)) & 0xFFu;
+                if (so < kMaxFood) {
+                    fobj[so] = make_float2((float)(xy & 15u) + bx, (float)(xy >> 4) + by);
+                    frot[so].x = __uint_as_float(rot[k]);
+                }
+                ++so;
+            }
+        }
+    }
+    if ((int)lane >= nf && (int)lane < na) fobj[lane] = make_float2(__builtin_nanf(""), __builtin_nanf(""));
+    wave_sync();
+    // every camera's heading (camera c in lane c % 64, register c / 64) and key
+    float hx[kG], hy[kG];
+#pragma unroll
+    for (int g = 0; g < kG; ++g) {
+        hx[g] = hy[g] = 0.0f;
+        const int c = 64 * g + (int)lane;
+        if (c < ncam) {
+            const int sl = F.cam[c];
+            heading(L.rw[sl], L.rz[sl], hx[g], hy[g]);
+            fkey[c] = kNoKey;
+        }
+    }
+    if ((int)lane < nf) frot[lane] = food_cs(__float_as_uint(frot[lane].x));
+    wave_sync();
+    if (ncam == 0) return;
+
+    // camera c's heading, from its lane (every lane shuffles)
+    auto head = [&](int c, float &ahx, float &ahy) {
+        ahx = __shfl(hx[0], c & 63);
+        ahy = __shfl(hy[0], c & 63);
+#pragma unroll
+        for (int g = 1; g < kG; ++g) {
+            const float gx = __shfl(hx[g], c & 63), gy = __shfl(hy[g], c & 63);
+            if ((c >> 6) == g) { ahx = gx; ahy = gy; }
+        }
+    };
+    const NearPt fnp = finder_np();
+    // the exact test of the queued pairs [q0, q0 + cntq), one per lane
+    auto exact = [&](int q0, int cntq) {
+        const int ln = (int)lane;
+        const uint32_t code = ln < cntq ? F.queue[q0 + ln] : 0u;
+        const int ic = (int)(code & 0xFFu), j = (int)(code >> 8);
+        const int sl = F.cam[ic];
+        float ahx, ahy;
+        head(ic, ahx, ahy);
+        if (ln < cntq) {
+            const bool food = j < na;
+            const float2 p = food ? fobj[j] : make_float2(L.x[j - na], L.y[j - na]);
+            // pair_fl / the oracle's raster: the exact (f, l)
+            const float vx = p.x - L.x[sl], vy = p.y - L.y[sl];
+            const float f = vx * ahx + vy * ahy;
+            const float l = vx * ahy - vy * ahx;
+            uint32_t kv;
+            if (food) {
+                const FoodBox b = box_setup(f, l, frot[j], make_float2(ahx, ahy));
+                kv = box_hit(b, 0.0f, true, fnp.c) ? zkey(box_z(b, true), kOrderFood + (uint32_t)j) : kNoKey;
+            } else {
+                kv = finder_key(f, l, kOrderAgent + (uint32_t)(j - na));
+            }
+            if (kv != kNoKey) atomicMin(&fkey[ic], kv);
+        }
+    };
+
+    // ---- the cull: lane = (camera a0 + a, object jb + o) ----
+    int nq = 0;
+    const int a = (int)lane >> 3, o = (int)lane & 7;
+    for (int a0 = 0; a0 < ncam; a0 += 8) {   // wave-uniform
+        const int nc = min(8, ncam - a0);
+        const int ic = a0 + min(a, nc - 1);
+        const int sl = F.cam[ic];
+        float ahx, ahy;
+        head(ic, ahx, ahy);
+        const float cxp = a < nc ? L.x[sl] : __builtin_nanf(""), cyp = L.y[sl];
+        // (P1's hoisted projections: f, l within ~1e-5, far inside the margins)
+        const float pc = __builtin_fmaf(cxp, ahx, cyp * ahy);
+        const float pd = __builtin_fmaf(cxp, ahy, -(cyp * ahx));
+        auto cull = [&](int j, float2 p, bool ok) {
+            const float f = __builtin_fmaf(p.x, ahx, __builtin_fmaf(p.y, ahy, -pc));
+            const float l = __builtin_fmaf(p.x, ahy, __builtin_fmaf(-p.y, ahx, -pd));
+            const bool keep = ok & (fabsf(l) <= kFinderCullL) & (f >= kFinderCullF);
+            const uint64_t m = ballot64(keep);
+            if (keep) F.queue[nq + (int)rank_below(m)] = (uint32_t)ic | ((uint32_t)j << 8);
+            nq += __popcll(m);
+            if (nq >= 64) {
+                wave_sync();
+                exact(nq - 64, 64);
+                wave_sync();
+                nq -= 64;
+            }
+        };
+        for (int jb = 0; jb < na; jb += 8) cull(jb + o, fobj[jb + o], true);
+        for (int jb = 0; jb < n0; jb += 8) {
+            const int t = min(jb + o, n0 - 1);
+            cull(na + jb + o, make_float2(L.x[t], L.y[t]), (jb + o < n0) & (jb + o != sl));
+        }
+    }
+    if (nq > 0) {
+        wave_sync();
+        exact(0, nq);
+    }
+    wave_sync();
+
+    // ---- per camera: the sensor's wall resolution of its finder ray ----
+#pragma unroll
+    for (int g = 0; g < kG; ++g) {
+        const int c = 64 * g + (int)lane;
+        if (c >= ncam) break;
+        const int sl = F.cam[c];
+        const uint32_t kv = fkey[c];
+        const uint32_t order = kv & kOrderMask;
+        const float z = __uint_as_float(kv & ~kOrderMask);
+        const float px = L.x[sl], py = L.y[sl];
+        const float ch_x = hx[g], ch_y = hy[g];
+        const float fx = fnp.c * ch_x + fnp.s * ch_y, fy = fnp.c * ch_y + fnp.s * (-ch_x);
+        const int fcls = wall_class(px + fx, py + fy);
+        const bool edge = !strictly_inside(px, py);
+        bool see;
+        if ((fcls != kWallInner) | edge)
+            see = (fcls == kWallNone) | ((fcls == kWallInner) && beats_wall(px, py, ch_x, ch_y, z));
+        else
+            see = beats_wall_in(kInLo - px, kInHiX - px, kInLo - py, kInHiY - py, ch_x, ch_y, z);
+        const bool agent = (kv != kNoKey) & (order >= kOrderAgent) & see;
+        L.finder[sl] = (int16_t)(agent ? (int32_t)(order - kOrderAgent) : -1);
+    }
+    wave_sync();
+}
+
+template <int kCap, bool kFinder>
+__device__ void world_step(SimState &S, const ObsTable &cur, WorldLDS<kCap> &L, FinderScratch<kCap> &F,
+                           uint32_t w, uint32_t lane)
 {
     constexpr int kG = kCap / 64;   // 64-slot groups
     const uint32_t cap = S.cap;
@@ -264,6 +463,12 @@ __device__ void world_step(SimState &S, const ObsTable &cur, WorldLDS<kCap> &L, 
     for (int g = 0; g < kG; ++g) rows[g] = -1;
     // per-world records: issued with the first batch (none depends on n0)
     const uint64_t food_rec = lane < kNumChunks ? S.food[(size_t)w * kNumChunks + lane] : 0ull;
+    // (kFinder) the food squares' rotations: the chunk's package 0 with the
+    // record, the others where the record says live
+    uint32_t frot_ld[kMaxPkg];
+#pragma unroll
+    for (int k = 0; k < kMaxPkg; ++k) frot_ld[k] = 0u;
+    if (kFinder && lane < kNumChunks) frot_ld[0] = S.food_rot[(size_t)w * kNumPkg + lane];
     const uint2 key = S.key[w];
     uint32_t ctr = S.ctr[w];
     int32_t cur_food = S.cur_food[w];
@@ -280,7 +485,9 @@ __device__ void world_step(SimState &S, const ObsTable &cur, WorldLDS<kCap> &L, 
         const float x = in ? S.x[i] : 0.0f, y = in ? S.y[i] : 0.0f;
         const float rw = in ? S.rw[i] : 0.0f, rz = in ? S.rz[i] : 0.0f;
         const int32_t sp = in ? S.species[i] : 0, hp = in ? S.health[i] : 0;
-        const int32_t fd = in ? S.finder[i] : -1;
+        // (kFinder: the finder slots are world_finders', not the last sensor's --
+        // except before any sensor ran, when S.finder holds the init's "none")
+        const int32_t fd = (in && (!kFinder || S.finder_from_state)) ? S.finder[i] : -1;
         if ((int)lane < n0) {
             rows[0] = row;
             if (row >= 0) {
@@ -309,15 +516,36 @@ __device__ void world_step(SimState &S, const ObsTable &cur, WorldLDS<kCap> &L, 
             L.rz[i] = S.rz[base + i];
             L.species[i] = (int8_t)S.species[base + i];
             L.accum[i] = S.health[base + i];
-            L.finder[i] = (int16_t)S.finder[base + i];
+            L.finder[i] = (kFinder && !S.finder_from_state) ? (int16_t)-1 : (int16_t)S.finder[base + i];
             L.flags[i] = (uint8_t)F_ALIVE;
         }
+    }
+    if (kFinder && lane < kNumChunks) {
+        const uint32_t lv = (uint32_t)(food_rec >> 40) & 31u;
+#pragma unroll
+        for (int k = 1; k < kMaxPkg; ++k)
+            if ((lv >> k) & 1u) frot_ld[k] = S.food_rot[(size_t)w * kNumPkg + k * kNumChunks + lane];
     }
     if (lane < kNumChunks) food_unpack(food_rec, &L.food[lane * kMaxPkg]);
     if (lane < kNumChunks) L.chunk[lane] = 0u;   // resetChunkInfoSystem
     if (lane < kNumSpecies) { L.cnt[lane] = 0u; L.hsum[lane] = 0u; L.scount[lane] = 0; }
     if (lane == 0) L.consumed = 0;
     wave_sync();
+    // the finder slots the shoot / breed actions read (kFinder: computed here)
+    if constexpr (kFinder) {
+        if (!S.finder_from_state) world_finders<kCap>(S, L, F, lane, n0, food_rec, frot_ld, (pa2.x | pa2.y) != 0);
+    }
+#ifdef MB_FINDER_CHECK   // debug build: the computed slots against the last sensor's (run serialised)
+    if (kFinder && !S.finder_from_state) {
+        for (int i = lane; i < n0; i += 64) {
+            const bool cam = i >= 64 || ((pa2.x | pa2.y) != 0);
+            const int mine = L.finder[i], sens = S.finder[base + i];
+            if (cam && mine != sens)
+                printf("FINDER w %u slot %d n0 %d mine %d sensor %d pos %.3f %.3f rot %.4f %.4f\n", w, i, n0, mine, sens,
+                       L.x[i], L.y[i], L.rw[i], L.rz[i]);
+        }
+    }
+#endif
 
     // ---- addFoodSystem (sim.cpp:363-387) + addFoodToChunk (:308-361) ----
     // The serial draw sequence uses at most 2 + 3 x 7 = 23 counters: lane k
@@ -482,7 +710,6 @@ __device__ void world_step(SimState &S, const ObsTable &cur, WorldLDS<kCap> &L, 
     }
     wave_sync();
     cur_food -= L.consumed;
-
     // ---- updateSurroundingObservation (sim.cpp:583-654) + tracker (:719-734) ----
     for (int i = lane; i < n1; i += 64) {
         if (!(L.flags[i] & F_ALIVE)) continue;
@@ -1008,6 +1235,10 @@ constexpr float kUEps = 2e-3f;                // root-interval margin in u
 constexpr float kFoodFar = 2.55f;
 constexpr float kCircleFar = 1.5f;
 constexpr float kFarCull = 5.0f;               // P1 angular cull from this |f| on
+constexpr float kInsideNear2 = 0.17f * 0.17f;  // disc centres this close are inside the near sphere
+#ifndef MB_NEAR_CULL
+#define MB_NEAR_CULL 1
+#endif
 #ifndef MB_SPLIT_FLUSH
 #define MB_SPLIT_FLUSH 16   // food survivors flushed alone from this many on (24: +0.2 %, 40: +0.3 %, never: +1 %)
 #endif
@@ -1180,7 +1411,14 @@ __device__ __forceinline__ void run_survivors(LDS &L, const RayTab &R, int na, i
         const bool food = j < na;
         const float r2 = f * f + l * l;
         if (fabsf(f) <= (food ? kFoodFar : kCircleFar)) {
-            wide = true;
+            // a disc whose centre lies within 0.17 of the camera is wholly inside
+            // the near sphere (0.17 + R = 1.09 < 1.1): no ray leaves it beyond
+            // 1.1, so no ray sees it -- the exact predicate's near point then
+            // lies >= 0.93 > R from the centre and the chord's midpoint < 0.17
+            // along the ray, margins of 1e-2 against float errors of 1e-6.
+            // Such pairs (a newborn on its parent, sim.cpp:561-564) skip the
+            // wide round.
+            wide = food | (r2 >= kInsideNear2) | !MB_NEAR_CULL;
         } else {
             // A far pair: the object lies on one side of the camera plane and
             // the near sphere clips none of its rays (circle: |f| > 1.5;
@@ -2225,14 +2463,15 @@ hipError_t launch_tile_sum(const SimState &S, int parity, hipStream_t st)
     hipLaunchKernelGGL(tile_sum_kernel, dim3(S.ntiles), dim3(1024), 0, st, S, parity);
     return hipGetLastError();
 }
-hipError_t launch_world_step(const SimState &S, const ObsTable &cur, int parity, hipStream_t st)
+hipError_t launch_world_step(const SimState &S, const ObsTable &cur, int parity, hipStream_t st, hipEvent_t done)
 {
-    if (S.cap <= 128)
-        hipLaunchKernelGGL(world_step_kernel<128>, dim3((S.W + kK1Worlds - 1) / kK1Worlds), dim3(64 * kK1Worlds), 0,
-                           st, S, cur, parity);
-    else
-        hipLaunchKernelGGL(world_step_kernel<256>, dim3((S.W + kK1Worlds - 1) / kK1Worlds), dim3(64 * kK1Worlds), 0,
-                           st, S, cur, parity);
+    const dim3 grid((S.W + kK1Worlds - 1) / kK1Worlds), blk(64 * kK1Worlds);
+    auto go = [&](auto kern) {
+        if (!done) hipLaunchKernelGGL(kern, grid, blk, 0, st, S, cur, parity);
+        else hipExtLaunchKernelGGL(kern, grid, blk, 0u, st, nullptr, done, 0u, S, cur, parity);   // on the packet
+    };
+    if (S.cap <= 128) S.k1_finder ? go(world_step_kernel<128, true>) : go(world_step_kernel<128, false>);
+    else S.k1_finder ? go(world_step_kernel<256, true>) : go(world_step_kernel<256, false>);
     return hipGetLastError();
 }
 hipError_t launch_scan(const SimState &S, int parity, hipStream_t st, hipEvent_t done, bool plain_events)

@@ -54,6 +54,13 @@ struct SimState {
     uint32_t *sig_fork;
     uint32_t epoch;
     uint32_t W, cap, A, world_offset, flags, seed, ntiles;
+    // K1 computes the finder slots its actions read itself (world_finders;
+    // small world counts) instead of reading the last sensor's S.finder, so it
+    // does not wait for that sensor
+    uint32_t k1_finder;
+    // ... except on the first step after init (no sensor has run: the finder
+    // slots are the init's "none", S.finder), set by the host for that launch
+    uint32_t finder_from_state;
     uint32_t Wx;                    // exported worlds: W, or W - 1 with the shard ghost (the
                                     // last world, its rows placed after every exported row)
 };
@@ -90,7 +97,8 @@ hipError_t launch_init(const SimState &S, hipStream_t st);
 hipError_t upload_ray_table(const SimState &S, hipStream_t st);
 hipError_t launch_tile_sum(const SimState &S, int parity, hipStream_t st);
 hipError_t launch_raise_flag(uint32_t *flag, uint32_t v, hipStream_t st);
-hipError_t launch_world_step(const SimState &S, const ObsTable &cur, int parity, hipStream_t st);
+hipError_t launch_world_step(const SimState &S, const ObsTable &cur, int parity, hipStream_t st,
+                             hipEvent_t done = nullptr);
 // plain_events: record `done` with hipEventRecord (stream capture) instead of on the dispatch
 hipError_t launch_scan(const SimState &S, int parity, hipStream_t st, hipEvent_t done = nullptr,
                        bool plain_events = false);

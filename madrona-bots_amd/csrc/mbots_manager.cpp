@@ -11,6 +11,9 @@
 //    rows (288 GB HBM per GPU leaves ample headroom);
 //  * the species-major export table is double-buffered: a step writes the new
 //    table while reading the old one (no in-place radix sort of 264-B rows).
+#if defined(MB_PROBE_NO_JOIN) && !defined(MB_PROBE_BUILD)
+#error "MB_PROBE_NO_JOIN gives wrong finder slots: a probe build (scripts/build_var.sh -DMB_PROBE_BUILD) only"
+#endif
 #include <hip/hip_ext.h>
 #include "../../include/mbots.h"
 #include "mbots_kernels.hpp"
@@ -82,6 +85,20 @@ struct mbots_handle {
     hipEvent_t ev_join[2] = {nullptr, nullptr};   // K3b of alternate steps done (aux)
     int last_join = -1;               // ev_join of the latest K3b, -1: none pending
     unsigned long long join_capture = 0;   // stream-capture id it was recorded in (0: none)
+    int prev_join = -1;               // ev_join of the K3b before it (its rows are the other
+                                      // table half's), -1: none
+    unsigned long long prev_capture = 0;
+    uint64_t join_serial[2] = {0, 0}; // the sensor launch (1, 2, ...) each ev_join marks
+    uint64_t sensor_serial = 0;       // sensors launched
+    uint64_t waited_serial = 0;       // the newest sensor the manager's stream order has waited
+                                      // for (outside graph capture; every call follows the last)
+    bool k1_finder = false;           // K1 computes the finder slots (small world counts):
+                                      // the next K1 does not wait for the sensor
+    bool sensed = false;              // a sensor has run since init (the finder slots are then
+                                      // the centre ray's, before it the init's "none")
+    int32_t *row_base2[2] = {nullptr, nullptr};   // row bases / sensor order of alternate
+    int32_t *sorder2[2] = {nullptr, nullptr};     // steps (a sensor may still read the last
+                                                  // step's while the next K2 writes)
     unsigned long long cap_seen = 0;  // the stream capture the last captured step belonged to
     uint64_t cap_steps = 0;           // steps recorded into it (mbots_join wants an even count)
     bool poisoned = false;            // a graph of an odd number of steps was captured: the
@@ -144,6 +161,13 @@ namespace {
 #ifndef MB_VALUE_ADAPT
 #define MB_VALUE_ADAPT 1   // value waits only while the host runs ahead of the device
 #endif
+// Up to this many worlds K1 computes the next step's finder slots itself
+// (world_finders), so the next K1 waits only for the caller's stream, not for
+// this step's sensor: the sensor chain and the caller chain of consecutive
+// steps overlap ("Small world counts")
+#ifndef MB_K1_FINDER_MAX
+#define MB_K1_FINDER_MAX 2048
+#endif
 // The runtime carries the wait as a polling kernel on the sensor's queue, which
 // spins until K2 (on the caller's queue) raises the flag: under a tool that runs
 // the device's kernels one at a time (rocprofv3 counter collection,
@@ -165,7 +189,10 @@ bool value_waits_safe()
     return true;
 }
 bool fork_by_value(uint32_t W) { return W <= MB_VALUE_FORK_MAX && value_waits_safe(); }
-bool join_by_value(uint32_t W) { return MB_VALUE_JOIN && W <= MB_VALUE_JOIN_MAX && value_waits_safe(); }
+bool join_by_value(uint32_t W)
+{
+    return MB_VALUE_JOIN && W <= MB_VALUE_JOIN_MAX && W > MB_K1_FINDER_MAX && value_waits_safe();
+}
 
 hipEvent_t get_event(mbots_handle *h)
 {
@@ -245,7 +272,9 @@ size_t layout(mbots_handle *h, Arena &a)
     S.cur_food = a.take<int32_t>(W);
     S.sreward = a.take<float>(W * kNumSpecies);
     S.scount = a.take<int32_t>(W * kNumSpecies);
-    S.row_base = a.take<int32_t>(W * kNumSpecies);
+    h->row_base2[0] = a.take<int32_t>(W * kNumSpecies);
+    h->row_base2[1] = a.take<int32_t>(W * kNumSpecies);
+    S.row_base = h->row_base2[0];
     S.world_off = a.take<int32_t>(W);
     S.src_of = a.take<int32_t>(rows);
     S.overflow = a.take<uint32_t>(W);
@@ -255,7 +284,12 @@ size_t layout(mbots_handle *h, Arena &a)
     S.tiles = a.take<int32_t>((size_t)2 * S.ntiles * kTileBuckets * 5);
     S.agent_steps = a.take<unsigned long long>(1);
     S.raytab = a.take<float4>(36);
-    S.sorder = sensor_order_used((uint32_t)W) ? a.take<int32_t>(W) : nullptr;
+    h->sorder2[0] = h->sorder2[1] = nullptr;
+    if (sensor_order_used((uint32_t)W)) {
+        h->sorder2[0] = a.take<int32_t>(W);
+        h->sorder2[1] = a.take<int32_t>(W);
+    }
+    S.sorder = h->sorder2[0];
     S.x_out = a.take<float>(rows);
     S.y_out = a.take<float>(rows);
     S.rw_out = a.take<float>(rows);
@@ -284,10 +318,34 @@ mbots::ObsTable src_view(const mbots_handle *h, int half)
     return t;
 }
 
+bool capturing(hipStream_t st);
 // make `st` wait for the last step's sensor (its rows, and the moves it did)
 int wait_sensor(mbots_handle *h, hipStream_t st)
 {
-    if (h->last_join >= 0) HIP_TRY(hipStreamWaitEvent(st, h->ev_join[h->last_join], 0));
+    if (h->last_join >= 0) {
+        HIP_TRY(hipStreamWaitEvent(st, h->ev_join[h->last_join], 0));
+        if (!capturing(st)) h->waited_serial = std::max(h->waited_serial, h->join_serial[h->last_join]);
+    }
+    return MBOTS_OK;
+}
+
+// make `st` wait for the sensor before the last one, whose rows are the other
+// table half's (the prev-sensor moves read them).  Only needed when K1 does
+// not wait for the sensors (k1_finder): otherwise the last step's K1 did.
+// (Under stream capture, only an event recorded in the same capture.)
+int wait_prev_sensor(mbots_handle *h, hipStream_t st)
+{
+    if (!h->k1_finder || h->prev_join < 0) return MBOTS_OK;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    unsigned long long cid = 0;
+    HIP_TRY(hipStreamGetCaptureInfo(st, &cs, &cid));
+    const bool cap = cs == hipStreamCaptureStatusActive;
+    if (cap && h->prev_capture != cid) return MBOTS_OK;
+    // (one cross-queue wait per step: the shift's for its prev-sensor rows
+    // covers the next K1's)
+    if (!cap && h->waited_serial >= h->join_serial[h->prev_join]) return MBOTS_OK;
+    HIP_TRY(hipStreamWaitEvent(st, h->ev_join[h->prev_join], 0));
+    if (!cap) h->waited_serial = std::max(h->waited_serial, h->join_serial[h->prev_join]);
     return MBOTS_OK;
 }
 
@@ -421,6 +479,7 @@ int materialize_psem(mbots_handle *h, hipStream_t st)
 {
     if (!h->psem_pending[h->tb]) return MBOTS_OK;
     HIP_TRY(hipSetDevice(h->device));
+    if (int rc = wait_prev_sensor(h, st)) return rc;   // its source rows are that sensor's
     const int rc = timed(h, MBOTS_TK_MOVE, st, [&] {
         return mbots::launch_move(h->S, h->T[h->tb ^ 1], h->T[h->tb], 0, mbots::kMoveSensor, st);
     });
@@ -488,10 +547,11 @@ struct CkptHeader {
     char magic[8];
     uint32_t version, num_worlds, cap, A, world_offset, flags, seed, n_rows;
     uint64_t bytes;
+    uint32_t sensed, pad;   // 4: whether a sensor had run (the finder slots are its)
 };
 // 3: totals[kTotRows] (every table row, the shard ghost's included) is part
-// of the state and must equal the header's n_rows
-constexpr uint32_t kCkptVersion = 3;
+// of the state and must equal the header's n_rows; 4: `sensed`
+constexpr uint32_t kCkptVersion = 4;
 
 struct Seg {
     void *p;
@@ -686,6 +746,8 @@ int mbots_create(const mbots_config *cfg_in, mbots_handle **out)
     S.world_offset = cfg.world_offset;
     S.flags = cfg.flags;
     S.seed = cfg.rand_seed;
+    h->k1_finder = S.W <= MB_K1_FINDER_MAX;
+    S.k1_finder = h->k1_finder ? 1u : 0u;
 
     int rc = MBOTS_OK;
     auto check = [&](hipError_t e, const char *what) {
@@ -848,10 +910,19 @@ int mbots_step(mbots_handle *h, void *stream)
     } else if (!capturing && (h->sig_fork || h->sig_join)) {
         ahead = true;
     }
-    if (!capturing && h->join_epoch != 0 && ahead)
+    const int before = h->last_join;                  // the last step's sensor (its rows are
+    const unsigned long long before_cap = h->join_capture;   // the current half's)
+    if (h->k1_finder) {
+        // K1 computed the finder slots this K1 reads; it must only not overwrite
+        // the state half the sensor before the last one may still read
+        if ((rc = wait_prev_sensor(h, st))) return rc;
+    } else if (!capturing && h->join_epoch != 0 && ahead) {
         HIP_TRY(hipStreamWaitValue32(st, h->sig_join, h->join_epoch, hipStreamWaitValueEq, 0xFFFFFFFFu));
-    else if (h->last_join >= 0 && (!capturing || h->join_capture == cap_id))
+    } else if (h->last_join >= 0 && (!capturing || h->join_capture == cap_id)) {
         HIP_TRY(hipStreamWaitEvent(st, h->ev_join[h->last_join], 0));
+        if (!capturing) h->waited_serial = std::max(h->waited_serial, h->join_serial[h->last_join]);
+    }
+    h->S.finder_from_state = h->sensed ? 0u : 1u;
     if ((rc = timed(h, MBOTS_TK_WORLD_STEP, st,
                     [&] { return mbots::launch_world_step(h->S, cur, par, st); })))
         return rc;
@@ -864,10 +935,22 @@ int mbots_step(mbots_handle *h, void *stream)
     // this step's epoch (under capture replays would repeat it: the event then)
     uint32_t epoch = 0;
     if ((h->sig_fork || h->sig_join) && !capturing && ahead) {
-        if (++h->epoch == 0) ++h->epoch;
-        epoch = h->epoch;
+        if (h->epoch >= 0x7FFFFFF0u) {
+            // the fork waits for "flag >= epoch": before the counter wraps, drain
+            // the device and restart both from 0
+            HIP_TRY(hipDeviceSynchronize());
+            if (h->sig_fork) HIP_TRY(hipMemset(h->sig_fork, 0, 8));
+            if (h->sig_join) HIP_TRY(hipMemset(h->sig_join, 0, 8));
+            h->epoch = 0;
+            h->join_epoch = 0;
+        }
+        epoch = ++h->epoch;
     }
     h->S.epoch = h->sig_fork ? epoch : 0u;
+    // this step's row bases and sensor order go to the buffer the step before
+    // last used (its sensor has been waited for: above, or by the event join)
+    h->S.row_base = h->row_base2[par];
+    h->S.sorder = h->sorder2[par];
     // this step's row counts are K2's: no host read of them before it (ADVICE r4:
     // cleared here, after every materialisation above that may sync the last ones)
     h->totals_ok = false;
@@ -880,12 +963,18 @@ int mbots_step(mbots_handle *h, void *stream)
     // none of which reads the sensor rows or the finder slots.  The next step's
     // K1 and the semantic/depth accessors wait for ev_join.
     const int jcur = h->last_join == 0 ? 1 : 0;
-    if (epoch && h->sig_fork) HIP_TRY(hipStreamWaitValue32(h->aux, h->sig_fork, epoch, hipStreamWaitValueEq, 0xFFFFFFFFu));
+    // (">=": with K1 not waiting for the sensors, the next step's K2 may raise
+    // its epoch before this queue reaches this wait)
+    if (epoch && h->sig_fork) HIP_TRY(hipStreamWaitValue32(h->aux, h->sig_fork, epoch, hipStreamWaitValueGte, 0xFFFFFFFFu));
     else HIP_TRY(hipStreamWaitEvent(h->aux, h->ev_totals, 0));
     if ((rc = timed(h, MBOTS_TK_SENSOR, h->aux, [&] {
              return mbots::launch_sensor(h->S, nxt, h->aux, h->ev_join[jcur], capturing);
          })))
         return rc;
+    h->sensed = true;
+    h->join_serial[jcur] = ++h->sensor_serial;
+    h->prev_join = before;
+    h->prev_capture = before_cap;
     h->last_join = jcur;
     h->join_capture = capturing ? cap_id : 0;
     h->join_epoch = 0;
@@ -896,6 +985,13 @@ int mbots_step(mbots_handle *h, void *stream)
     if ((rc = timed(h, MBOTS_TK_EXPORT, st,
                     [&] { return mbots::launch_export_rows(h->S, nxt, 0, st); })))
         return rc;
+    // (the prev-sensor part reads the last step's sensor rows; K1 waited for
+    // that sensor unless it computed the finder slots itself)
+    if ((prefetch & mbots::kMoveSensor) && h->k1_finder && before >= 0 && (!capturing || before_cap == cap_id) &&
+        (capturing || h->waited_serial < h->join_serial[before])) {
+        HIP_TRY(hipStreamWaitEvent(st, h->ev_join[before], 0));
+        if (!capturing) h->waited_serial = std::max(h->waited_serial, h->join_serial[before]);
+    }
     if (prefetch && (rc = timed(h, MBOTS_TK_MOVE, st, [&] {
                          return mbots::launch_move(h->S, cur, nxt, lazy, prefetch, st);
                      })))
@@ -943,6 +1039,7 @@ int mbots_shift_observations(mbots_handle *h, void *stream)
     const bool with_psem = fused && h->psem_pending[tb];
     if (fused) {
         const mbots::ObsTable src = src_view(h, tb ^ 1);
+        if (with_psem && (rc = wait_prev_sensor(h, st))) return rc;   // the prev sensor's source rows
         rc = timed(h, MBOTS_TK_SHIFT, st, [&] {
             return mbots::launch_move(h->S, src, h->T[tb], 0,
                                       mbots::kMoveAHShift | (with_psem ? mbots::kMoveSensor : 0), st);
@@ -1435,6 +1532,7 @@ int mbots_save_checkpoint(mbots_handle *h, void *dst, uint64_t bytes)
     hd.seed = h->cfg.rand_seed;
     hd.n_rows = n_rows;
     hd.bytes = need;
+    hd.sensed = h->sensed ? 1u : 0u;
     char *p = static_cast<char *>(dst);
     memcpy(p, &hd, sizeof(hd));
     p += sizeof(hd);
@@ -1496,6 +1594,8 @@ int mbots_load_checkpoint(mbots_handle *h, const void *src, uint64_t bytes)
     h->tb = 0;
     h->parity = 0;
     h->last_join = -1;
+    h->prev_join = -1;
+    h->waited_serial = h->sensor_serial;   // (the device is idle)
     h->join_epoch = 0;
     h->prev_lazy[0] = h->prev_lazy[1] = false;
     h->ah_pending[0] = h->ah_pending[1] = false;
@@ -1506,6 +1606,7 @@ int mbots_load_checkpoint(mbots_handle *h, const void *src, uint64_t bytes)
     h->forced = 0;
     h->prefetched = 0;
     h->steps = 1;
+    h->sensed = hd.sensed != 0;
     hipStream_t st = nullptr;
     h->last_stream = st;
     h->totals_ok = false;

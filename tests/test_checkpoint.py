@@ -155,7 +155,7 @@ def test_set_action_after_step_then_shift():
 def test_checkpoint_load_then_save_before_stepping(ghost):
     """a restored manager saved again before any step writes the
     same blob (the table's row count -- every row, the shard ghost's included,
-    kCkptVersion 3 -- comes back with the state), and an older version's blob
+    kCkptVersion 3+ -- comes back with the state), and an older version's blob
     is refused."""
     import madrona_bots as mb
     kw = dict(shard_ghost=ghost)
@@ -185,10 +185,10 @@ def test_checkpoint_with_bad_totals_leaves_manager_intact():
     b = mb.SimManager(0, 64, 5, 32)
     _run(b, 0, 2)
     mine = b.save_checkpoint()
-    # header (48 B), 11 agent columns of 64 x 128 slots, the per-world arrays
+    # header (56 B), 11 agent columns of 64 x 128 slots, the per-world arrays
     # (n, ctr, key, food, food_rot, cur_food, sreward, scount, row_base,
     # world_off, overflow: 1420 B per world), then totals[8]
-    tot = 48 + 11 * 64 * 128 * 4 + 64 * 1420
+    tot = 56 + 11 * 64 * 128 * 4 + 64 * 1420
     assert int(np.frombuffer(blob[tot + 20:tot + 24].tobytes(), np.uint32)[0]) == a.num_rows()
     bad = blob.copy()
     bad[tot + 20:tot + 24] = np.frombuffer(np.uint32(a.num_rows() + 1).tobytes(), np.uint8)
