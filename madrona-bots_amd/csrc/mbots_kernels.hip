@@ -407,10 +407,27 @@ __device__ void world_finders(const SimState &S, WorldLDS<kCap> &L, FinderScratc
                 nq -= 64;
             }
         };
-        for (int jb = 0; jb < na; jb += 8) cull(jb + o, fobj[jb + o], true);
-        for (int jb = 0; jb < n0; jb += 8) {
-            const int t = min(jb + o, n0 - 1);
-            cull(na + jb + o, make_float2(L.x[t], L.y[t]), (jb + o < n0) & (jb + o != sl));
+        // (each iteration's object loaded one iteration ahead: the LDS latency
+        // overlaps the previous pair's tests instead of stalling each one)
+        if (na > 0) {
+            float2 pn = fobj[o];
+            for (int jb = 0; jb < na; jb += 8) {
+                const float2 p = pn;
+                if (jb + 8 < na) pn = fobj[jb + 8 + o];
+                cull(jb + o, p, true);
+            }
+        }
+        {
+            int tn = min(o, n0 - 1);
+            float2 pn = make_float2(L.x[tn], L.y[tn]);
+            for (int jb = 0; jb < n0; jb += 8) {
+                const float2 p = pn;
+                if (jb + 8 < n0) {
+                    tn = min(jb + 8 + o, n0 - 1);
+                    pn = make_float2(L.x[tn], L.y[tn]);
+                }
+                cull(na + jb + o, p, (jb + o < n0) & (jb + o != sl));
+            }
         }
     }
     if (nq > 0) {
@@ -1663,6 +1680,36 @@ __global__ __launch_bounds__(64 * kWaves, sensor_min_waves(kCap)) void sensor_ke
         rows[g] = sp == 1 ? rb.x + c1 + (int)rank_below(m1) : sp == 2 ? rb.y + c2 + (int)rank_below(m2)
                 : sp == 3 ? rb.z + c3 + (int)rank_below(m3) : rb.w + c4 + (int)rank_below(m4);
         c1 += __popcll(m1); c2 += __popcll(m2); c3 += __popcll(m3); c4 += __popcll(m4);
+    }
+    // (K1-finder mode: the step's prev-sensor move, updateSensorOutputIdx
+    // sim.cpp:736-789, done here -- each slot's last row is K1's obsrow_out,
+    // the last sensor's rows precede this one on its stream -- so the caller's
+    // stream needs no wait for that sensor; the first wave of a world does it)
+    if (S.psem_src != nullptr && (kSplit == 1 || wv % kSplit == 0)) {
+#pragma unroll
+        for (int g = 0; g < kG; ++g) {
+            const int i = 64 * g + (int)lane;
+            if (i < n) {
+                const int32_t o = S.obsrow_out[base + i];
+                const size_t r = (size_t)rows[g];
+                uint4 a = make_uint4(0u, 0u, 0u, 0u), b = a;
+                if (o >= 0) {
+                    a = reinterpret_cast<const uint4 *>(S.psem_src + (size_t)o * kSensor)[0];
+                    b = reinterpret_cast<const uint4 *>(S.psem_src + (size_t)o * kSensor)[1];
+                }
+                reinterpret_cast<uint4 *>(nxt.psem + r * kSensor)[0] = a;
+                reinterpret_cast<uint4 *>(nxt.psem + r * kSensor)[1] = b;
+                if (depth) {
+                    uint4 c = make_uint4(0u, 0u, 0u, 0u), d = c;
+                    if (o >= 0) {
+                        c = reinterpret_cast<const uint4 *>(S.pdepth_src + (size_t)o * kSensor)[0];
+                        d = reinterpret_cast<const uint4 *>(S.pdepth_src + (size_t)o * kSensor)[1];
+                    }
+                    reinterpret_cast<uint4 *>(nxt.pdepth + r * kSensor)[0] = c;
+                    reinterpret_cast<uint4 *>(nxt.pdepth + r * kSensor)[1] = d;
+                }
+            }
+        }
     }
     const int nobj = na + n;
     // sentinels past the last object: a NaN position fails every P1 test, so

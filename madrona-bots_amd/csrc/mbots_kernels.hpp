@@ -61,6 +61,10 @@ struct SimState {
     // ... except on the first step after init (no sensor has run: the finder
     // slots are the init's "none", S.finder), set by the host for that launch
     uint32_t finder_from_state;
+    // (K1-finder mode) the last table's sensor rows: the sensor itself moves
+    // them into its rows' prev-sensor columns (null: the shift / moves do)
+    const int8_t *psem_src;
+    const uint8_t *pdepth_src;
     uint32_t Wx;                    // exported worlds: W, or W - 1 with the shard ghost (the
                                     // last world, its rows placed after every exported row)
 };

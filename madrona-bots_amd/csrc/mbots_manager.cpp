@@ -883,7 +883,7 @@ int mbots_step(mbots_handle *h, void *stream)
     // observation and PrevHiddenState between step and shift, as
     // training_loop.py:47-88 does): moved right after this step's K3a, beside
     // the sensor, instead of behind the wait for it (DESIGN.md "Prefetch")
-    const int prefetch = h->forced;
+    int prefetch = h->forced;
     h->forced = 0;
     h->prefetched = prefetch;
     // no shift since the last step: its deferred Prev moves first
@@ -967,10 +967,19 @@ int mbots_step(mbots_handle *h, void *stream)
     // its epoch before this queue reaches this wait)
     if (epoch && h->sig_fork) HIP_TRY(hipStreamWaitValue32(h->aux, h->sig_fork, epoch, hipStreamWaitValueGte, 0xFFFFFFFFu));
     else HIP_TRY(hipStreamWaitEvent(h->aux, h->ev_totals, 0));
-    if ((rc = timed(h, MBOTS_TK_SENSOR, h->aux, [&] {
-             return mbots::launch_sensor(h->S, nxt, h->aux, h->ev_join[jcur], capturing);
-         })))
-        return rc;
+    // (K1-finder mode: the sensor also moves the last table's sensor rows into
+    // its rows' prev-sensor columns, so no caller-stream wait is needed for them)
+    const bool psem_by_sensor = h->k1_finder;
+    if (psem_by_sensor) {
+        h->S.psem_src = h->T[h->tb].sem;
+        h->S.pdepth_src = (h->cfg.flags & MBOTS_FLAG_FIX_DEPTH_ALIAS) ? h->T[h->tb].depth : nullptr;
+    }
+    rc = timed(h, MBOTS_TK_SENSOR, h->aux, [&] {
+        return mbots::launch_sensor(h->S, nxt, h->aux, h->ev_join[jcur], capturing);
+    });
+    h->S.psem_src = nullptr;
+    h->S.pdepth_src = nullptr;
+    if (rc) return rc;
     h->sensed = true;
     h->join_serial[jcur] = ++h->sensor_serial;
     h->prev_join = before;
@@ -985,13 +994,8 @@ int mbots_step(mbots_handle *h, void *stream)
     if ((rc = timed(h, MBOTS_TK_EXPORT, st,
                     [&] { return mbots::launch_export_rows(h->S, nxt, 0, st); })))
         return rc;
-    // (the prev-sensor part reads the last step's sensor rows; K1 waited for
-    // that sensor unless it computed the finder slots itself)
-    if ((prefetch & mbots::kMoveSensor) && h->k1_finder && before >= 0 && (!capturing || before_cap == cap_id) &&
-        (capturing || h->waited_serial < h->join_serial[before])) {
-        HIP_TRY(hipStreamWaitEvent(st, h->ev_join[before], 0));
-        if (!capturing) h->waited_serial = std::max(h->waited_serial, h->join_serial[before]);
-    }
+    // (the prev sensor is the sensor's own part in K1-finder mode)
+    if (psem_by_sensor) prefetch &= ~mbots::kMoveSensor;
     if (prefetch && (rc = timed(h, MBOTS_TK_MOVE, st, [&] {
                          return mbots::launch_move(h->S, cur, nxt, lazy, prefetch, st);
                      })))
@@ -1004,7 +1008,7 @@ int mbots_step(mbots_handle *h, void *stream)
     h->prev_lazy[nt] = false;
     h->a_alias[nt] = h->h_alias[nt] = false;
     h->cur_ah_pending[nt] = true;
-    h->psem_pending[nt] = true;
+    h->psem_pending[nt] = !psem_by_sensor;
     h->ah_pending[nt] = true;
     h->six_pending[nt] = true;
     h->six_lazy[nt] = lazy != 0;
@@ -1111,6 +1115,7 @@ int mbots_export_on(mbots_handle *h, int32_t id, void *stream, mbots_tensor *out
     case MBOTS_EXPORT_PREV_SENSOR_SEMANTIC: case MBOTS_EXPORT_PREV_SENSOR_DEPTH:
         need = mbots::kMoveSensor;
         if ((rc = materialize_psem(h, st))) return rc;
+        if (h->k1_finder && (rc = wait_sensor(h, st))) return rc;   // the sensor moved them
         break;
     default: break;
     }
@@ -1256,7 +1261,8 @@ int mbots_construct_obs(mbots_handle *h, int32_t prev, float *out, uint64_t out_
     int rc = use_stream(h, st);
     if (rc) return rc;
     const int owed = pending_mask(h);
-    if (!prev && (rc = wait_sensor(h, st))) return rc;   // current semantic rows come from K3b
+    // current semantic rows come from K3b (and in K1-finder mode the prev ones too)
+    if ((!prev || h->k1_finder) && (rc = wait_sensor(h, st))) return rc;
     // The previous rows' health / position / surrounding: while the step's
     // deferred move of the six Prev* columns is still owed, gathered from the
     // other half along src_of inside this launch (what the move would write,
