@@ -15,12 +15,12 @@ for W in ${WORLDS:-65536 4096}; do
   bash scripts/ab_libs.sh ${ROUNDS:-3} $libs -- --worlds $W --steps ${STEPS:-100} --warmup ${WARM:-200} > gpurun_out/ab_${TAG:-a}_$W.log 2>&1 || { tail -5 gpurun_out/ab_${TAG:-a}_$W.log; exit 1; }
   python - $W ${TAG:-a} <<'PY'
 import json, collections, sys
-r = collections.defaultdict(list)
+r = collections.defaultdict(list); hr = collections.defaultdict(list)
 for line in open(f"gpurun_out/ab_{sys.argv[2]}_{sys.argv[1]}.log"):
     if line.startswith("{"):
-        d = json.loads(line); r[d["lib"]].append(d["ms_per_step"])
+        d = json.loads(line); r[d["lib"]].append(d["ms_per_step"]); hr[d["lib"]].append(d.get("host_ms_per_step", 0))
 for k, v in r.items():
-    print(f"W={sys.argv[1]} {k:28s} ms/step " + " ".join(f"{x:.4f}" for x in v) + f"   min {min(v):.4f}")
+    print(f"W={sys.argv[1]} {k:28s} ms/step " + " ".join(f"{x:.4f}" for x in v) + f"   min {min(v):.4f}  host {min(hr[k]):.4f}")
 PY
 done
 if [ -n "${PHASES:-}" ]; then

@@ -12,7 +12,7 @@ mkdir -p gpurun_out
 TAG=${TAG:-r04}
 for n in ${RANKS:-2 4}; do
   timeout -k 10 300 python -u bench.py --gpus $n --backend gloo --same-device --steps 40 --warmup 10 \
-      --worlds ${WORLDS:-16384} --no-secondary --no-cpu-baseline > gpurun_out/${TAG}_multi$n.log 2>&1 \
+      --worlds ${WORLDS:-16384} $([ -z "${SECONDARY:-}" ] && echo --no-secondary) --no-cpu-baseline > gpurun_out/${TAG}_multi$n.log 2>&1 \
       || { tail -5 gpurun_out/${TAG}_multi$n.log; exit 1; }
   grep '^{' gpurun_out/${TAG}_multi$n.log | tail -1 > gpurun_out/${TAG}_rehearsal_${n}rank_same_device.json
   python -c "import json; d = json.load(open('gpurun_out/${TAG}_rehearsal_${n}rank_same_device.json')); c = d.get('config5', {}); print($n, 'ranks:', round(d['ms_per_step'], 4), 'ms/step; config5', c.get('ms_per_step'), c.get('error'))"

@@ -31,11 +31,13 @@ s0 = m.agent_steps()
 t0 = time.perf_counter()
 for t in range(a.warmup, a.warmup + a.steps):
     m.step(); m.shift_observations(); m.write_synthetic_actions(1234, t + 1)
+th = time.perf_counter() - t0   # the host's enqueue time (= dt when host-bound)
 torch.cuda.synchronize()
 dt = time.perf_counter() - t0
 kt = m.kernel_times()
 out = {"lib": os.path.basename(os.environ.get("MBOTS_LIB", "default")),
        "stream_priority": a.stream_priority,
        "agent_steps_per_s": (m.agent_steps() - s0) / dt, "ms_per_step": dt / a.steps * 1e3,
+       "host_ms_per_step": th / a.steps * 1e3,
        "kernel_ms": {k: round(v[0] / v[1], 4) for k, v in kt.items() if v[1]}}
 print(json.dumps(out), flush=True)
