@@ -54,6 +54,7 @@ SEED = 69                   # learn/env.py:15
 ACTION_SEED = 1234
 AGENTS_PER_WORLD = 32       # learn/env.py:15
 CONFIG4_WORLDS = 262144     # BASELINE config 4 (sharded across 8 GPUs)
+CONFIG5_WORLDS = 262144     # BASELINE config 5 (the learner round trip over 8 GPUs)
 STEADY_FROM, STEADY_STEPS = 250, 100   # the steady-state line: food at its cap
 
 
@@ -340,7 +341,7 @@ def spawn_ranks(args):
     return subprocess.run(cmd, env=env).returncode
 
 
-def config5_loop(mgr, args, rank, world_size, dev, distributed):
+def config5_loop(main_mgr, args, rank, world_size, dev, distributed):
     """BASELINE config 5: every rank steps its shard; after each step what the
     learner reads (learn/training_loop.py:43-93: current and previous
     observation columns, reward, stats, Action, HiddenState, PrevHiddenState)
@@ -350,9 +351,17 @@ def config5_loop(mgr, args, rank, world_size, dev, distributed):
     out of scope: random one-hot actions, memory from the gathered hidden
     state); shift; the actions and memory go back to the ranks that own the
     rows (scatter_actions, :136-137).  Wall clock of the timed steps, max over
-    ranks; returns the line's dict on rank 0."""
+    ranks; returns the line's dict on rank 0.  Its own shards: BASELINE config
+    5's 262144 worlds in all, 262144 / N per rank (the main line's manager when
+    N does not divide it)."""
     import gather
     import madrona_bots as mb
+    if CONFIG5_WORLDS % world_size == 0:
+        W5 = CONFIG5_WORLDS // world_size
+        mgr = mb.SimManager(dev.index, W5, SEED, AGENTS_PER_WORLD, world_offset=rank * W5,
+                            shard_ghost=rank < world_size - 1)
+    else:
+        mgr, W5 = main_mgr, main_mgr.num_worlds
     steps = max(10, args.steps // 2)
     gsec = [0.0, 0.0]
     nrows = [0]
@@ -400,16 +409,18 @@ def config5_loop(mgr, args, rank, world_size, dev, distributed):
         dist.barrier()
         dist.all_reduce(st, op=dist.ReduceOp.MAX)
     el, gs, ss = (float(x) for x in st.tolist())
+    rb = mgr.learner_record_bytes()
+    del mgr
     if rank != 0:
         return None
     rows = nrows[0] / steps
-    rb = mgr.learner_record_bytes()
     return {"what": "step + learner records (current and previous observation columns, reward, stats, Action, "
                     f"HiddenState, PrevHiddenState: {rb} B/agent) gathered to rank 0 and unpacked there + "
                     "actions / memory chosen there + shift + actions / memory scattered back to the owning ranks "
                     "(harness/gather.py gather_learner / scatter_actions)",
             "backend": args.backend if distributed else "none (one rank: pack + unpack + write locally)",
-            "n_gpus": world_size, "steps": steps, "ms_per_step": el / steps * 1e3,
+            "n_gpus": world_size, "worlds_per_gpu": W5, "total_worlds": W5 * world_size,
+            "steps": steps, "ms_per_step": el / steps * 1e3,
             "value": rows / (el / steps), "unit": "agent-steps/s (every rank's agents through the learner round trip)",
             "gather_ms_per_step": gs / steps * 1e3, "scatter_ms_per_step": ss / steps * 1e3,
             "rows_per_step_at_learner": rows,
