@@ -12,7 +12,7 @@ if [ -n "${K:-}" ]; then
 fi
 libs="madrona-bots_amd/madrona_bots/libmbots.so $(ls build_var/libmbots_*.so 2>/dev/null)"
 for W in ${WORLDS:-65536 4096}; do
-  bash scripts/ab_libs.sh ${ROUNDS:-3} $libs -- --worlds $W --steps ${STEPS:-100} --warmup ${WARM:-200} > gpurun_out/ab_${TAG:-a}_$W.log 2>&1 || { tail -5 gpurun_out/ab_${TAG:-a}_$W.log; exit 1; }
+  bash scripts/ab_libs.sh ${ROUNDS:-3} $libs -- --worlds $W --steps ${STEPS:-100} --warmup ${WARM:-200} ${KB_EXTRA:-} > gpurun_out/ab_${TAG:-a}_$W.log 2>&1 || { tail -5 gpurun_out/ab_${TAG:-a}_$W.log; exit 1; }
   python - $W ${TAG:-a} <<'PY'
 import json, collections, sys
 r = collections.defaultdict(list); hr = collections.defaultdict(list)
