@@ -1024,8 +1024,10 @@ __global__ __launch_bounds__(1024) void tile_sum_kernel(SimState S, int parity)
 // updateSensorOutputIdx sim.cpp:736-789) is recorded in src_of[new_row] for
 // the K4 move stream.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void export_rows_kernel(SimState S, ObsTable nxt, int init)
+template <bool kInit>
+__global__ __launch_bounds__(256) void export_rows_kernel(SimState S, ObsTable nxt)
 {
+    constexpr bool init = kInit;
     const uint32_t wv = threadIdx.x >> 6;
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t w = uniform(blockIdx.x * kWorldsPerBlock + wv);
@@ -1045,6 +1047,23 @@ __global__ __launch_bounds__(256) void export_rows_kernel(SimState S, ObsTable n
         const int i = b + (int)lane;
         const bool active = i < n;
         const int32_t sp = active ? (b == 0 ? sp0 : S.species[base + i]) : 0;
+        // every column of the slot loaded with its species (one memory round
+        // trip per 64 slots: the wave holds its slot for less time beside the
+        // sensor)
+        float x = 0.0f, y = 0.0f, s0 = 0.0f, s1 = 0.0f;
+        int32_t h = 0, old = -1;
+        uint32_t st = 0u;
+        if (active) {
+            x = S.x[base + i];
+            y = S.y[base + i];
+            h = S.health[base + i];
+            if (!init) {
+                s0 = S.sur0[base + i];
+                s1 = S.sur1[base + i];
+                st = S.stats[base + i];
+            }
+            old = S.obsrow_out[base + i];
+        }
         const uint64_t m1 = ballot64(sp == 1), m2 = ballot64(sp == 2);
         const uint64_t m3 = ballot64(sp == 3), m4 = ballot64(sp == 4);
         int32_t row = 0;
@@ -1056,14 +1075,9 @@ __global__ __launch_bounds__(256) void export_rows_kernel(SimState S, ObsTable n
         carry2 += __popcll(m3); carry3 += __popcll(m4);
         if (!active) continue;
         const size_t r = (size_t)row;
-        const float x = S.x[base + i], y = S.y[base + i];
-        const int32_t h = S.health[base + i];
-        const float s0 = init ? 0.0f : S.sur0[base + i];
-        const float s1 = init ? 0.0f : S.sur1[base + i];
-        const uint32_t st = init ? 0u : S.stats[base + i];
         // old row: K1's obsrow_out (the sensor reads it beside this kernel);
         // the new row goes to obsrow, which the next K1 reads
-        S.src_of[r] = S.obsrow_out[base + i];
+        S.src_of[r] = old;
         S.obsrow[base + i] = row;
         constexpr bool nt = (MB_NT & 4) != 0;
         st_stream(nxt.species + r, sp, nt);
@@ -2538,7 +2552,8 @@ hipError_t launch_scan(const SimState &S, int parity, hipStream_t st, hipEvent_t
 }
 hipError_t launch_export_rows(const SimState &S, const ObsTable &nxt, int init, hipStream_t st)
 {
-    hipLaunchKernelGGL(export_rows_kernel, dim3(world_blocks(S.W)), dim3(256), 0, st, S, nxt, init);
+    if (init) hipLaunchKernelGGL(export_rows_kernel<true>, dim3(world_blocks(S.W)), dim3(256), 0, st, S, nxt);
+    else hipLaunchKernelGGL(export_rows_kernel<false>, dim3(world_blocks(S.W)), dim3(256), 0, st, S, nxt);
     return hipGetLastError();
 }
 hipError_t launch_move(const SimState &S, const ObsTable &cur, const ObsTable &nxt, int prev_lazy,
