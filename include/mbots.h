@@ -302,7 +302,9 @@ const char *mbots_last_error(void);
 /* Environment.
  * MBOTS_VALUE_FORK=0: the step's cross-stream hops (K1 -> the sensor's
  *   internal stream, and the sensor back to the next step) are event waits.
- *   Otherwise, at <= 8192 worlds and while the host runs ahead of the device,
+ *   Otherwise, from 2049 to 8192 worlds and while the host runs ahead of the
+ *   device (up to 2048 the next step's K1 computes the finder slots itself and
+ *   does not wait for the sensor; the fork is then an event wait),
  *   they are hipStreamWaitValue32 waits on signal words a kernel stores (about
  *   3 us instead of 7 per hop).  The runtime carries such a wait as a polling
  *   kernel on the waiting stream; a tool or mode that runs the device's
