@@ -3,12 +3,17 @@
  * manager in MBOTS_EXEC_CPU mode, step / shift it with the identity-keyed
  * action stream, and print a digest of the exported views.
  * tests/test_c_host.py builds it with gcc -std=c99 -pedantic -Werror and
- * compares the digest with the same calls made through madrona_bots. */
+ * compares the digest with the same calls made through madrona_bots; built
+ * with -DMBOTS_HOST_HIP (and the HIP runtime) it also runs MBOTS_EXEC_HIP
+ * (argument "hip"), copying each device view to the host for the digest. */
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
 #include "mbots.h"
+#ifdef MBOTS_HOST_HIP
+#include <hip/hip_runtime_api.h>
+#endif
 
 #define CHECK(call)                                                              \
     do {                                                                         \
@@ -39,6 +44,7 @@ int main(int argc, char **argv)
 {
     const uint32_t worlds = argc > 1 ? (uint32_t)atoi(argv[1]) : 16u;
     const uint32_t steps = argc > 2 ? (uint32_t)atoi(argv[2]) : 6u;
+    const int32_t mode = argc > 3 && strcmp(argv[3], "hip") == 0 ? MBOTS_EXEC_HIP : MBOTS_EXEC_CPU;
     static const int32_t ids[] = {MBOTS_EXPORT_ACTION, MBOTS_EXPORT_REWARD, MBOTS_EXPORT_POSITION,
                                   MBOTS_EXPORT_PREV_POSITION, MBOTS_EXPORT_HEALTH,
                                   MBOTS_EXPORT_SURROUNDING, MBOTS_EXPORT_SENSOR_SEMANTIC,
@@ -62,6 +68,7 @@ int main(int argc, char **argv)
     }
 
     cfg.num_worlds = worlds;
+    cfg.exec_mode = mode;
     cfg.rand_seed = 69;
     cfg.init_num_agents_per_world = 32;
     CHECK(mbots_create(&cfg, &h));
@@ -72,12 +79,30 @@ int main(int argc, char **argv)
     }
     CHECK(mbots_num_agents(h, &n));
     for (k = 0; k < sizeof(ids) / sizeof(ids[0]); ++k) {
+        size_t bytes;
         CHECK(mbots_export(h, ids[k], &t));
-        if (t.device != -1) {
-            fprintf(stderr, "export %d: not a host view in CPU mode\n", ids[k]);
+        bytes = (size_t)(t.dims[0] * t.dims[1]) * elem_size(t.dtype);
+        if ((t.device == -1) != (mode == MBOTS_EXEC_CPU)) {
+            fprintf(stderr, "export %d: device %d in mode %d\n", ids[k], t.device, mode);
             return 1;
         }
-        digest = fnv1a(t.data, (size_t)(t.dims[0] * t.dims[1]) * elem_size(t.dtype), digest);
+        if (t.device == -1) {
+            digest = fnv1a(t.data, bytes, digest);
+        } else {
+#ifdef MBOTS_HOST_HIP
+            /* mbots_export returns once the view's data is final */
+            void *buf = malloc(bytes ? bytes : 1u);
+            if (!buf || hipMemcpy(buf, t.data, bytes, hipMemcpyDeviceToHost) != hipSuccess) {
+                fprintf(stderr, "hipMemcpy of export %d failed\n", ids[k]);
+                return 1;
+            }
+            digest = fnv1a(buf, bytes, digest);
+            free(buf);
+#else
+            fprintf(stderr, "built without MBOTS_HOST_HIP\n");
+            return 1;
+#endif
+        }
     }
     CHECK(mbots_destroy(h));
     printf("agents %u digest %016llx\n", n, (unsigned long long)digest);

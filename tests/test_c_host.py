@@ -50,3 +50,21 @@ def test_c_host_matches_python_surface(tmp_path):
             m.shift_observations()
     assert out[:2] == ["agents", str(m.num_agents())]
     assert int(out[3], 16) == _fnv1a(_views(m))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("W", [16, 4100])
+def test_c_host_hip_equals_cpu(tmp_path, W):
+    """The same C host on MBOTS_EXEC_HIP (device views copied out with
+    hipMemcpy) prints the CPU mode's digest: K1-finder mode at 16 worlds, the
+    joined schedule with its value waits at 4100."""
+    exe = tmp_path / "host_hip"
+    subprocess.run(["gcc", "-std=c99", "-Wall", "-O1", "-D__HIP_PLATFORM_AMD__", "-DMBOTS_HOST_HIP",
+                    "-I", os.path.join(ROOT, "include"), "-I", "/opt/rocm/include",
+                    os.path.join(ROOT, "tests", "c_host", "host.c"),
+                    "-L", LIBDIR, "-lmbots", "-L", "/opt/rocm/lib", "-lamdhip64",
+                    "-Wl,-rpath," + LIBDIR + ":/opt/rocm/lib", "-o", str(exe)], check=True)
+    run = lambda mode: subprocess.run([str(exe), str(W), "8", mode], check=True, capture_output=True,
+                                      text=True, timeout=120).stdout.split()
+    cpu, hip = run("cpu"), run("hip")
+    assert hip == cpu, (hip, cpu)
