@@ -121,6 +121,10 @@ struct mbots_handle {
     bool prev_lazy[2] = {false, false};   // table half's six shift-owned Prev* columns are
                                           // still its current ones (lazy shift, K5)
     hipEvent_t ev_hop = nullptr;      // orders a call's stream after the last one used
+    // MBOTS_SWAP=1 (large world counts): K1 and K2 on the sensor's stream, the
+    // caller's stream joining after K2 (DESIGN.md 4 "Which chain sets the pace")
+    bool swap = false;
+    hipEvent_t ev_caller = nullptr;   // the caller's stream at a step's start
     uint32_t *sig_fork = nullptr;     // the fork's signal word (small world counts)
     uint32_t *sig_join = nullptr;     // the join's (raised after the sensor)
     uint32_t epoch = 0;               // the last epoch K2 raised (never 0)
@@ -787,6 +791,9 @@ int mbots_create(const mbots_config *cfg_in, mbots_handle **out)
         if (join_by_value((uint32_t)S.W)) signal_word(h->sig_join);
         S.sig_fork = h->sig_fork;
     }
+    if (const char *e = std::getenv("MBOTS_SWAP"))
+        h->swap = e[0] == '1' && S.W > MB_VALUE_FORK_MAX && !h->k1_finder && !h->sig_fork && !h->sig_join;
+    if (h->swap) check(hipEventCreateWithFlags(&h->ev_caller, kSyncEvent), "hipEventCreateWithFlags");
     check(hipEventCreateWithFlags(&h->ev_join[0], kSyncEvent), "hipEventCreateWithFlags");
     check(hipEventCreateWithFlags(&h->ev_join[1], kSyncEvent), "hipEventCreateWithFlags");
     {
@@ -838,6 +845,7 @@ int mbots_destroy(mbots_handle *h)
     for (auto e : h->pool) (void)hipEventDestroy(e);
     if (h->ev_totals) (void)hipEventDestroy(h->ev_totals);
     if (h->ev_hop) (void)hipEventDestroy(h->ev_hop);
+    if (h->ev_caller) (void)hipEventDestroy(h->ev_caller);
     if (h->sig_fork) (void)hipFree(h->sig_fork);
     if (h->sig_join) (void)hipFree(h->sig_join);
     for (auto e : h->ev_join) if (e) (void)hipEventDestroy(e);
@@ -921,7 +929,15 @@ int mbots_step(mbots_handle *h, void *stream)
     }
     const int before = h->last_join;                  // the last step's sensor (its rows are
     const unsigned long long before_cap = h->join_capture;   // the current half's)
-    if (h->k1_finder) {
+    // MBOTS_SWAP=1: K1, K2 and the sensor on the internal stream with no hop
+    // between them; K1 after the last sensor (the same stream) and after what
+    // the caller enqueued so far (the learner's writes)
+    const bool swap = h->swap && !capturing;
+    const hipStream_t kst = swap ? h->aux : st;
+    if (swap) {
+        HIP_TRY(hipEventRecord(h->ev_caller, st));
+        HIP_TRY(hipStreamWaitEvent(h->aux, h->ev_caller, 0));
+    } else if (h->k1_finder) {
         // K1 computed the finder slots this K1 reads; it must only not overwrite
         // the state half the sensor before the last one may still read
         if ((rc = wait_prev_sensor(h, st))) return rc;
@@ -932,8 +948,8 @@ int mbots_step(mbots_handle *h, void *stream)
         if (!capturing) h->waited_serial = std::max(h->waited_serial, h->join_serial[h->last_join]);
     }
     h->S.finder_from_state = h->sensed ? 0u : 1u;
-    if ((rc = timed(h, MBOTS_TK_WORLD_STEP, st,
-                    [&] { return mbots::launch_world_step(h->S, cur, par, st); })))
+    if ((rc = timed(h, MBOTS_TK_WORLD_STEP, kst,
+                    [&] { return mbots::launch_world_step(h->S, cur, par, kst); })))
         return rc;
     mbots::swap_state(h->S);
     // K2 writes the row counts into the pinned mirror; accessors and the
@@ -963,7 +979,7 @@ int mbots_step(mbots_handle *h, void *stream)
     // this step's row counts are K2's: no host read of them before it (ADVICE r4:
     // cleared here, after every materialisation above that may sync the last ones)
     h->totals_ok = false;
-    rc = timed(h, MBOTS_TK_SCAN, st, [&] { return mbots::launch_scan(h->S, par, st, h->ev_totals, capturing); });
+    rc = timed(h, MBOTS_TK_SCAN, kst, [&] { return mbots::launch_scan(h->S, par, kst, h->ev_totals, capturing); });
     h->S.epoch = 0;
     if (rc) return rc;
     // fork after K2: the K3b sensor (VALU-bound; it derives the export rows from
@@ -974,7 +990,8 @@ int mbots_step(mbots_handle *h, void *stream)
     const int jcur = h->last_join == 0 ? 1 : 0;
     // (">=": with K1 not waiting for the sensors, the next step's K2 may raise
     // its epoch before this queue reaches this wait)
-    if (epoch && h->sig_fork) HIP_TRY(hipStreamWaitValue32(h->aux, h->sig_fork, epoch, hipStreamWaitValueGte, 0xFFFFFFFFu));
+    if (swap) HIP_TRY(hipStreamWaitEvent(st, h->ev_totals, 0));   // K3a after K2 (the caller's join)
+    else if (epoch && h->sig_fork) HIP_TRY(hipStreamWaitValue32(h->aux, h->sig_fork, epoch, hipStreamWaitValueGte, 0xFFFFFFFFu));
     else HIP_TRY(hipStreamWaitEvent(h->aux, h->ev_totals, 0));
     // (K1-finder mode: the sensor also moves the last table's sensor rows into
     // its rows' prev-sensor columns, so no caller-stream wait is needed for them)

@@ -16,7 +16,7 @@ import pytest
 import torch
 
 import pyoracle
-from simpair import compare
+from simpair import COLUMNS, compare
 
 pytestmark = pytest.mark.gpu
 
@@ -202,3 +202,40 @@ def test_config5_rollout_records_two_shards_equal_one(fix_depth):
         assert torch.equal(got[k].view(torch.int32), want[k].contiguous().view(torch.int32)), k
     # the records hold what the learner needs at 64 B/agent against 280 B of f32 rows + reward
     assert full.pack_rollout().numel() == full.num_agents() * rb
+
+
+@pytest.mark.gpu
+def test_schedules_agree_16384_worlds(monkeypatch):
+    """The step's two schedules at large world counts -- K1 / K2 on the
+    caller's stream with the sensor forked off (the default), and K1 / K2 /
+    the sensor on the internal stream with the caller joining after K2
+    (MBOTS_SWAP=1) -- give the same tables, and the oracle's, over 60 steps of
+    16384 worlds."""
+    import madrona_bots as mb
+    W, T = 16384, 60
+    mgrs = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("MBOTS_SWAP", mode)   # read when the manager is created
+        mgrs[mode] = mb.SimManager(0, W, 69, 32)
+    monkeypatch.delenv("MBOTS_SWAP", raising=False)
+    orc = pyoracle.OracleSim(W, 69, 32, num_threads=16)
+    for t in range(T):
+        wh = t % 3 == 0
+        for m in mgrs.values():
+            m.write_synthetic_actions(1234, t, wh)
+            m.step()
+            m.shift_observations()
+        orc.write_synthetic_actions(1234, t, wh)
+        orc.step()
+        orc.shift_observations()
+        if t % 20 == 19:
+            ref = mgrs["0"]
+            for mode in ("1",):
+                for name, _ in COLUMNS:
+                    for prev in (False, True):
+                        a = getattr(ref, name)(prev).to_torch()
+                        b = getattr(mgrs[mode], name)(prev).to_torch()
+                        assert a.shape == b.shape and torch.equal(a.view(torch.uint8), b.view(torch.uint8)), \
+                            (t, mode, name, prev)
+    errs = compare(mgrs["0"], orc, "end")
+    assert not errs, errs[:5]
