@@ -296,6 +296,12 @@ enum mbots_timed_kernel {
 int mbots_enable_kernel_timing(mbots_handle *h, int32_t enable);
 int mbots_kernel_times(mbots_handle *h, double ms[MBOTS_TK_COUNT],
                        uint64_t launches[MBOTS_TK_COUNT]);
+/* The step schedule the manager chose (diagnostics, no device call):
+ * out[0] flags -- 1 K1-finder mode (the next K1 does not wait for the last
+ * sensor), 2 fork by value, 4 join by value, 8 MBOTS_SWAP; out[1] the last
+ * value-wait epoch raised; out[2] how often the epochs restarted from 0;
+ * out[3] steps run.  CPU mode: all 0 but out[3]. */
+int mbots_schedule_info(mbots_handle *h, uint32_t out[4]);
 
 const char *mbots_last_error(void);
 
@@ -320,7 +326,10 @@ const char *mbots_last_error(void);
  *   world's food at its cap), slower early in a run (+0.6 to +1.2 % over steps
  *   5-24), so it is off by default.
  * MBOTS_CPU_THREADS: host threads of MBOTS_EXEC_CPU (default: the machine's
- *   hardware threads, at most 16). */
+ *   hardware threads, at most 16).
+ * MBOTS_EPOCH_START=<n> (read at mbots_create; a test hook): the value waits
+ *   count their epochs on from n (at most 0x7FFFFFF0, where they restart
+ *   from 0 after draining the device), so a short run crosses the restart. */
 #define MBOTS_SERIALISING_ENV \
     { "ROCPROF_COUNTER_COLLECTION", "HSA_TOOLS_LIB", "ROCP_INPUT", "AMD_SERIALIZE_KERNEL", \
       "AMD_SERIALIZE_COPY" }

@@ -46,7 +46,10 @@ struct SimState {
     float *x_out, *y_out, *rw_out, *rz_out;
     int32_t *species_out, *n_out;
     int32_t *obsrow_out;            // K1 -> K3a / the sensor: each slot's old export row (not
-                                    // swapped: K1 reads obsrow, K3a rewrites it)
+                                    // swapped with obsrow -- K1 reads obsrow, K3a rewrites it --
+                                    // but one of two buffers by step parity, set by the host:
+                                    // in K1-finder mode the sensor of step t reads it beside
+                                    // step t+1's K1)
     uint64_t *food_out;
     // the fork as a value wait (small world counts, mbots_step): K2's last
     // block stores `epoch` into sig_fork (signal memory); epoch 0: no flag

@@ -99,7 +99,11 @@ struct mbots_handle {
     int32_t *row_base2[2] = {nullptr, nullptr};   // row bases / sensor order of alternate
     int32_t *sorder2[2] = {nullptr, nullptr};     // steps (a sensor may still read the last
                                                   // step's while the next K2 writes)
+    int32_t *obsrow_out2[2] = {nullptr, nullptr}; // K1's old-row column of alternate steps (in
+                                                  // K1-finder mode the sensor reads the last
+                                                  // step's while the next K1 writes)
     unsigned long long cap_seen = 0;  // the stream capture the last captured step belonged to
+    hipStream_t cap_stream = nullptr; // the stream it was recorded on (live while capturing)
     uint64_t cap_steps = 0;           // steps recorded into it (mbots_join wants an even count)
     bool poisoned = false;            // a graph of an odd number of steps was captured: the
                                       // host's table bookkeeping no longer follows the device
@@ -128,6 +132,7 @@ struct mbots_handle {
     uint32_t *sig_fork = nullptr;     // the fork's signal word (small world counts)
     uint32_t *sig_join = nullptr;     // the join's (raised after the sensor)
     uint32_t epoch = 0;               // the last epoch K2 raised (never 0)
+    uint32_t epoch_wraps = 0;         // times the epochs restarted from 0 (kEpochWrap)
     uint32_t join_epoch = 0;          // the epoch raised after the last sensor (0: none;
                                       // the join is then the sensor's event)
     bool totals_ok = false;           // h_totals holds the last step's counts (synchronised)
@@ -180,6 +185,8 @@ namespace {
 // the device's kernels one at a time (rocprofv3 counter collection,
 // AMD_SERIALIZE_KERNEL) the poller can be dispatched first and never end, so
 // those keep the event wait (as does MBOTS_VALUE_FORK=0).
+// the value waits' epochs restart from 0 once they reach this (mbots_step)
+constexpr uint32_t kEpochWrap = 0x7FFFFFF0u;
 bool env_set(const char *name)
 {
     const char *v = std::getenv(name);
@@ -305,7 +312,9 @@ size_t layout(mbots_handle *h, Arena &a)
     S.rw_out = a.take<float>(rows);
     S.rz_out = a.take<float>(rows);
     S.species_out = a.take<int32_t>(rows);
-    S.obsrow_out = a.take<int32_t>(rows);
+    h->obsrow_out2[0] = a.take<int32_t>(rows);
+    h->obsrow_out2[1] = a.take<int32_t>(rows);
+    S.obsrow_out = h->obsrow_out2[0];
     S.n_out = a.take<int32_t>(W);
     S.food_out = a.take<uint64_t>(W * kNumChunks);
     fill_table(h->T[0], a, rows);
@@ -370,6 +379,20 @@ bool capturing(hipStream_t st)
 // (ADVICE r3/r4): every device entry point refuses to run from then on --
 // checked here (use_stream, sync_totals and the entry points that use neither)
 // and by mbots_step when the next capture starts.
+// (only a capture that has ENDED with an odd count poisons; a call
+// on another stream while the capture is still recording is refused alone)
+bool capture_open(const mbots_handle *h)
+{
+    if (!h->cap_stream || !h->cap_seen) return false;
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    unsigned long long cid = 0;
+    if (hipStreamGetCaptureInfo(h->cap_stream, &cs, &cid) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return cs == hipStreamCaptureStatusActive && cid == h->cap_seen;
+}
+
 int capture_guard(mbots_handle *h, hipStream_t st)
 {
     static const char *kMsg = "the last graph capture recorded an odd number of steps, so the manager's "
@@ -377,6 +400,10 @@ int capture_guard(mbots_handle *h, hipStream_t st)
                               "(ending with join()) and create a new manager";
     if (h->poisoned) return fail(MBOTS_E_INVALID, kMsg);
     if ((h->cap_steps & 1) && !capturing(st)) {
+        if (capture_open(h))
+            return fail(MBOTS_E_INVALID, "a graph capture of this manager's steps is still recording on another "
+                                         "stream: call the manager on the capturing stream, or after the "
+                                         "capture has ended");
         h->poisoned = true;
         return fail(MBOTS_E_INVALID, kMsg);
     }
@@ -790,6 +817,10 @@ int mbots_create(const mbots_config *cfg_in, mbots_handle **out)
         if (fork_by_value((uint32_t)S.W)) signal_word(h->sig_fork);
         if (join_by_value((uint32_t)S.W)) signal_word(h->sig_join);
         S.sig_fork = h->sig_fork;
+        // test hook: the epoch to count on from (near kEpochWrap, so a short
+        // run crosses the wrap; include/mbots.h "Environment")
+        if (const char *e = std::getenv("MBOTS_EPOCH_START"))
+            h->epoch = std::min<uint32_t>((uint32_t)std::strtoul(e, nullptr, 0), kEpochWrap);
     }
     if (const char *e = std::getenv("MBOTS_SWAP"))
         h->swap = e[0] == '1' && S.W > MB_VALUE_FORK_MAX && !h->k1_finder && !h->sig_fork && !h->sig_join;
@@ -876,6 +907,7 @@ int mbots_step(mbots_handle *h, void *stream)
     if (!h) return fail(MBOTS_E_INVALID, "null handle");
     if (h->cpu) {
         h->cpu->step();
+        ++h->steps;
         return capacity_report(h, (uint32_t)std::min<uint64_t>(h->cpu->overflow(), 0xFFFFFFFFu));
     }
     HIP_TRY(hipSetDevice(h->device));
@@ -889,6 +921,7 @@ int mbots_step(mbots_handle *h, void *stream)
         // a new capture: the previous one must have held an even number of steps
         if ((rc = capture_guard(h, nullptr))) return rc;
         h->cap_seen = cap_id;
+        h->cap_stream = st;
         h->cap_steps = 0;
     }
     if ((rc = use_stream(h, st))) return rc;
@@ -942,12 +975,20 @@ int mbots_step(mbots_handle *h, void *stream)
         // the state half the sensor before the last one may still read
         if ((rc = wait_prev_sensor(h, st))) return rc;
     } else if (!capturing && h->join_epoch != 0 && ahead) {
-        HIP_TRY(hipStreamWaitValue32(st, h->sig_join, h->join_epoch, hipStreamWaitValueEq, 0xFFFFFFFFu));
+        // ">=" (VERDICT r5 item 5): the flag only grows -- one writer, raised in
+        // step order on the sensor's queue -- so this wait passes whenever it is
+        // reached, even after a later step has raised the flag again; an
+        // equality wait would hang there (the round-5 probe's fork did)
+        HIP_TRY(hipStreamWaitValue32(st, h->sig_join, h->join_epoch, hipStreamWaitValueGte, 0xFFFFFFFFu));
     } else if (h->last_join >= 0 && (!capturing || h->join_capture == cap_id)) {
         HIP_TRY(hipStreamWaitEvent(st, h->ev_join[h->last_join], 0));
         if (!capturing) h->waited_serial = std::max(h->waited_serial, h->join_serial[h->last_join]);
     }
     h->S.finder_from_state = h->sensed ? 0u : 1u;
+    // K1 writes this step's old rows into the half the step before last used:
+    // the sensor that read it (K1-finder mode: the sensor before the last one)
+    // has been waited for above
+    h->S.obsrow_out = h->obsrow_out2[par];
     if ((rc = timed(h, MBOTS_TK_WORLD_STEP, kst,
                     [&] { return mbots::launch_world_step(h->S, cur, par, kst); })))
         return rc;
@@ -960,14 +1001,19 @@ int mbots_step(mbots_handle *h, void *stream)
     // this step's epoch (under capture replays would repeat it: the event then)
     uint32_t epoch = 0;
     if ((h->sig_fork || h->sig_join) && !capturing && ahead) {
-        if (h->epoch >= 0x7FFFFFF0u) {
-            // the fork waits for "flag >= epoch": before the counter wraps, drain
-            // the device and restart both from 0
+        if (h->epoch >= kEpochWrap) {
+            // both waits are "flag >= epoch": before the counter wraps, drain
+            // the device and restart both from 0 -- the resets complete before
+            // any later wait is enqueued (exercised by
+            // tests/test_robustness.py::test_value_wait_epoch_wrap through
+            // MBOTS_EPOCH_START)
             HIP_TRY(hipDeviceSynchronize());
             if (h->sig_fork) HIP_TRY(hipMemset(h->sig_fork, 0, 8));
             if (h->sig_join) HIP_TRY(hipMemset(h->sig_join, 0, 8));
+            HIP_TRY(hipDeviceSynchronize());
             h->epoch = 0;
             h->join_epoch = 0;
+            ++h->epoch_wraps;
         }
         epoch = ++h->epoch;
     }
@@ -988,8 +1034,10 @@ int mbots_step(mbots_handle *h, void *stream)
     // none of which reads the sensor rows or the finder slots.  The next step's
     // K1 and the semantic/depth accessors wait for ev_join.
     const int jcur = h->last_join == 0 ? 1 : 0;
-    // (">=": with K1 not waiting for the sensors, the next step's K2 may raise
-    // its epoch before this queue reaches this wait)
+    // (">=": the fork flag only grows -- K2's last block raises each step's
+    // epoch in step order -- so the wait passes whenever the sensor's queue
+    // reaches it, also after a later K2 raised the flag again; equality would
+    // hang there)
     if (swap) HIP_TRY(hipStreamWaitEvent(st, h->ev_totals, 0));   // K3a after K2 (the caller's join)
     else if (epoch && h->sig_fork) HIP_TRY(hipStreamWaitValue32(h->aux, h->sig_fork, epoch, hipStreamWaitValueGte, 0xFFFFFFFFu));
     else HIP_TRY(hipStreamWaitEvent(h->aux, h->ev_totals, 0));
@@ -1692,6 +1740,21 @@ int mbots_enable_kernel_timing(mbots_handle *h, int32_t enable)
     h->pending.clear();
     for (int k = 0; k < MBOTS_TK_COUNT; ++k) { h->acc_ms[k] = 0.0; h->acc_n[k] = 0; }
     h->timing = enable != 0;
+    return MBOTS_OK;
+}
+
+int mbots_schedule_info(mbots_handle *h, uint32_t out[4])
+{
+    if (!h || !out) return fail(MBOTS_E_INVALID, "null argument");
+    if (h->cpu) {
+        out[0] = out[1] = out[2] = 0;
+        out[3] = (uint32_t)h->steps;
+        return MBOTS_OK;
+    }
+    out[0] = (h->k1_finder ? 1u : 0u) | (h->sig_fork ? 2u : 0u) | (h->sig_join ? 4u : 0u) | (h->swap ? 8u : 0u);
+    out[1] = h->epoch;
+    out[2] = h->epoch_wraps;
+    out[3] = (uint32_t)h->steps;
     return MBOTS_OK;
 }
 

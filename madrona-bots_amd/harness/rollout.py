@@ -92,6 +92,86 @@ def random_rollout(sim, steps, seed=1234, shift_per_species=False, device=None, 
     return stats
 
 
+def learner_rollout(sim, steps, seed=1234, shift_per_species=True, fused=False, record=None, gen=None,
+                    end_of_step=None):
+    """The exact view pattern of learn/training_loop.py:36-137 with a learner
+    stand-in instead of the models (out of scope):
+
+        step(); species offsets (:43-45); action_tensor(False) and
+        hidden_state_tensor(False) fetched ONCE (:47-48); reward / health
+        clones (:49-50); per species: construct_obs(cur) (:57), its memory
+        rows (:58), construct_obs(prev) (:87), PrevHiddenState rows (:89), the
+        previous actions' argmax (:93); shift_observations() (:135, once per
+        species -- SURVEY B.9 -- unless shift_per_species=False); then the new
+        one-hot actions and memory written through the views taken before the
+        shifts (:136-137).
+
+    The stand-in's actions are torch.randint draws and its memory
+    prev_memory * 0.5 + randn (both exact in float32 on any device), all drawn
+    from one CPU generator, so a HIP manager and the oracle adapter given the
+    same seed take the same decisions while their tables agree.  fused=True
+    builds the observation rows with sim.construct_obs (one launch for all
+    species) where the reference's torch.cat would read the same columns.
+    `record(t, sp, name, tensor)`, when given, receives every tensor the loop
+    reads (what the learner would consume), for comparison between runs;
+    `end_of_step(t)` runs after each step's writes; `gen` continues the draws
+    of an earlier call (a CPU torch.Generator) instead of seeding a new one."""
+    if gen is None:
+        gen = torch.Generator(device="cpu").manual_seed(seed)
+    rec = record if record is not None else (lambda *a: None)
+    agent_steps = 0
+    for t in range(steps):
+        sim.step()
+        offsets = species_offsets(sim)
+        action_tensor = sim.action_tensor(False).to_torch()
+        memory_tensor = sim.hidden_state_tensor(False).to_torch()
+        all_rewards = sim.reward_tensor(False).to_torch().clone()
+        all_healths = sim.health_tensor(False).to_torch().clone()
+        rec(t, -1, "reward", all_rewards)
+        rec(t, -1, "health", all_healths)
+        if fused:
+            obs_all = sim.construct_obs(False)
+            prev_all = sim.construct_obs(True)
+        writes = []
+        for sp, (s, e) in enumerate(offsets):
+            if fused and not (shift_per_species and sp > 0):
+                obs = obs_all[s:e]
+            else:   # (after a per-species shift the fused rows are stale: rebuild)
+                obs = construct_obs(sim, s, e, prev=False)
+            prev_memory = memory_tensor[s:e, :]
+            rec(t, sp, "obs", obs)
+            rec(t, sp, "prev_memory", prev_memory)
+            a = torch.randint(0, ACTION_DIM, (e - s,), generator=gen)
+            noise = torch.randn((e - s, prev_memory.shape[1]), generator=gen)
+            new_memory = prev_memory * 0.5 + noise.to(prev_memory.device)
+            one_hot = torch.zeros(e - s, ACTION_DIM, dtype=torch.int32, device=action_tensor.device)
+            one_hot.scatter_(1, a.to(action_tensor.device).unsqueeze(1), 1)
+            if fused and not (shift_per_species and sp > 0):
+                prev_obs = prev_all[s:e]
+            else:
+                prev_obs = construct_obs(sim, s, e, prev=True)
+            og_hidden = sim.hidden_state_tensor(True).to_torch()[s:e, :]
+            prev_actions = action_tensor[s:e, :].argmax(dim=1)
+            rec(t, sp, "prev_obs", prev_obs)
+            rec(t, sp, "og_hidden", og_hidden)
+            rec(t, sp, "prev_actions", prev_actions)
+            if shift_per_species:
+                sim.shift_observations()
+                action_tensor[s:e, :] = one_hot
+                memory_tensor[s:e, :] = new_memory
+            else:
+                writes.append((s, e, one_hot, new_memory))
+        if not shift_per_species:
+            sim.shift_observations()
+            for s, e, one_hot, new_memory in writes:
+                action_tensor[s:e, :] = one_hot
+                memory_tensor[s:e, :] = new_memory
+        agent_steps += offsets[-1][1]
+        if end_of_step is not None:
+            end_of_step(t)
+    return {"steps": steps, "agent_steps": agent_steps}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--worlds", type=int, default=4096)

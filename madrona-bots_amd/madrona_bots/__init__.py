@@ -25,8 +25,8 @@ import warnings
 
 import torch  # loads the HIP runtime libmbots.so links against (same soname)
 
-__all__ = ["SimManager", "Tensor", "madrona", "ExportID", "ExecMode", "unpack_rollout", "unpack_learner",
-           "CapacityWarning", "CapacityError", "MAX_CAPACITY"]
+__all__ = ["SimManager", "ScriptBotsViewer", "Tensor", "madrona", "ExportID", "ExecMode", "unpack_rollout",
+           "unpack_learner", "CapacityWarning", "CapacityError", "MAX_CAPACITY"]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB_PATH = os.path.join(_HERE, "libmbots.so")
@@ -89,6 +89,7 @@ def _load():
         "mbots_overflow": [vp, P(ctypes.c_uint64)],
         "mbots_enable_kernel_timing": [vp, i32],
         "mbots_kernel_times": [vp, P(ctypes.c_double), P(ctypes.c_uint64)],
+        "mbots_schedule_info": [vp, P(u32)],
     }
     for name, args in sig.items():
         fn = getattr(L, name)
@@ -643,9 +644,40 @@ class SimManager:
     def enable_kernel_timing(self, enable=True):
         _check(_lib.mbots_enable_kernel_timing(self._h, 1 if enable else 0))
 
+    def schedule_info(self):
+        """The step schedule in use (mbots_schedule_info): {"k1_finder",
+        "fork_by_value", "join_by_value", "swap": bool, "epoch", "epoch_wraps",
+        "steps": int}."""
+        v = (ctypes.c_uint32 * 4)()
+        _check(_lib.mbots_schedule_info(self._h, v))
+        f = v[0]
+        return {"k1_finder": bool(f & 1), "fork_by_value": bool(f & 2), "join_by_value": bool(f & 4),
+                "swap": bool(f & 8), "epoch": int(v[1]), "epoch_wraps": int(v[2]), "steps": int(v[3])}
+
     def kernel_times(self):
         """{kernel: (total_ms, launches)} since enable_kernel_timing()."""
         ms = (ctypes.c_double * len(KERNELS))()
         n = (ctypes.c_uint64 * len(KERNELS))()
         _check(_lib.mbots_kernel_times(self._h, ms, n))
         return {k: (ms[i], n[i]) for i, k in enumerate(KERNELS)}
+
+
+class ScriptBotsViewer:
+    """The reference module's second class (src/entry/entry.cpp:47-80): a
+    windowed viewer around a Manager (src/gfx, Vulkan) whose ``loop(num_epochs,
+    step_fn, carry)`` calls ``step_fn(epoch, carry)`` once per rendered frame
+    and whose ``get_sim_mgr()`` returns the manager.  The viewer is out of this
+    build's scope, so the name exists
+    for the reference's imports -- ``from madrona_bots import SimManager,
+    ScriptBotsViewer`` (learn/training_loop.py:8, learn/env_app.py:2,
+    learn/app.py:1) -- and constructing it raises.  Headless training takes the
+    training loop's other branch (``TrainLoopManager`` over ``SimManager``,
+    training_loop.py:15-26, :172-173); ``SimManager.world_state`` /
+    ``dump_worlds`` replace the viewer's readback for offline inspection."""
+
+    def __init__(self, gpu_id, num_worlds, rand_seed, init_num_agents_per_world, window_width,
+                 window_height):
+        raise NotImplementedError(
+            "madrona_bots: ScriptBotsViewer (the reference's Vulkan viewer, src/gfx) is not part of this "
+            "build; run headless with SimManager (learn/training_loop.py without --enable_viewer) and "
+            "inspect worlds with SimManager.world_state() / dump_worlds()")

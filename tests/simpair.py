@@ -62,4 +62,7 @@ def compare(mgr, orc, where, prev_too=True, depth_fixed=False):
         do = orc.column(pyoracle.COL_SEMANTIC).view(np.uint8)
     if not np.array_equal(dg, do):
         errs.append(f"{where}: depth_tensor differs")
+    if depth_fixed and prev_too:   # (aliased, the prev depth is the prev semantic above)
+        if not np.array_equal(gpu_column(mgr, "depth_tensor", True), orc.column(pyoracle.COL_DEPTH, True)):
+            errs.append(f"{where}: depth_tensor(prev=True) differs")
     return errs

@@ -129,3 +129,85 @@ def test_value_waits_off_under_serialised_dispatch():
     p = subprocess.run([sys.executable, "-u", os.path.join(HERE, "serialised_child.py"), "4096", "10"],
                        env=env, capture_output=True, text=True, timeout=120)
     assert p.returncode == 0 and "OK" in p.stdout, (p.returncode, p.stdout[-2000:], p.stderr[-2000:])
+
+
+def test_schedule_info_cpu():
+    import madrona_bots as mb
+    m = mb.SimManager(0, 8, 69, 32, exec_mode="cpu")
+    for _ in range(3):
+        m.step()
+    info = m.schedule_info()
+    assert info["steps"] == 3 and not any(info[k] for k in ("k1_finder", "fork_by_value", "swap"))
+
+
+@pytest.mark.gpu
+def test_value_wait_epoch_wrap(monkeypatch):
+    """the value waits' epochs restart from 0 at 0x7FFFFFF0
+    (drain the device, clear both signal words, synchronise, count on from 1).
+    MBOTS_EPOCH_START starts a 4096-world manager (fork and join by value) a
+    few epochs short of the restart; 20 steps of the bench's loop with no host
+    read in between -- so the host runs ahead and every step takes the value
+    waits -- cross it, and the tables equal the oracle's, then again after
+    more steps."""
+    import madrona_bots as mb
+    W = 4096
+    monkeypatch.setenv("MBOTS_EPOCH_START", str(0x7FFFFFF0 - 6))
+    mgr = mb.SimManager(0, W, 69, 32)
+    monkeypatch.delenv("MBOTS_EPOCH_START")
+    info = mgr.schedule_info()
+    assert info["fork_by_value"] and info["join_by_value"] and info["epoch"] == 0x7FFFFFF0 - 6
+    orc = pyoracle.OracleSim(W, 69, 32, num_threads=8)
+    t = 0
+    for burst in (20, 5):
+        # a spin kernel first, so the host enqueues the whole burst while the
+        # device is still busy: every step sees the last sensor unfinished
+        torch.cuda._sleep(20_000_000)
+        for k in range(burst):
+            mgr.write_synthetic_actions(1234, t + k, True)
+            mgr.step()
+            mgr.shift_observations()
+        for k in range(burst):
+            orc.write_synthetic_actions(1234, t + k, True)
+            orc.step()
+            orc.shift_observations()
+        t += burst
+        errs = compare(mgr, orc, f"after {t} steps")
+        assert not errs, errs[:5]
+    info = mgr.schedule_info()
+    assert info["epoch_wraps"] == 1 and 0 < info["epoch"] < 64, info
+
+
+@pytest.mark.gpu
+def test_capture_guard_refuses_other_stream_without_poisoning():
+    """a call on another stream while a capture of the manager's
+    steps is still recording (an odd count so far) is refused on its own; the
+    capture then ends with an even count and the manager keeps working.  A
+    capture that ENDS with an odd count still poisons the manager
+    (tests/test_parity_gpu.py)."""
+    import madrona_bots as mb
+    W = 64
+    mgr = mb.SimManager(0, W, 69, 32)
+    orc = pyoracle.OracleSim(W, 69, 32, num_threads=8)
+    s, other = torch.cuda.Stream(), torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s):
+        mgr.write_synthetic_actions(1234, 0)
+        orc.write_synthetic_actions(1234, 0)
+        mgr.step(); orc.step()
+        mgr.shift_observations(); orc.shift_observations()
+        mgr.write_synthetic_actions(1234, 1)
+        orc.write_synthetic_actions(1234, 1)
+        torch.cuda.synchronize()
+        with torch.cuda.graph(g, stream=s, capture_error_mode="relaxed"):
+            mgr.step(); mgr.shift_observations(); mgr.write_synthetic_actions(1234, 2)
+            with torch.cuda.stream(other):
+                with pytest.raises(RuntimeError, match="still recording"):
+                    mgr.write_synthetic_actions(1234, 9)
+            mgr.step(); mgr.shift_observations(); mgr.write_synthetic_actions(1234, 3)
+            mgr.join()
+    g.replay()
+    for t in (2, 3):
+        orc.step(); orc.shift_observations(); orc.write_synthetic_actions(1234, t)
+    errs = compare(mgr, orc, "after the capture")
+    assert not errs, errs[:5]
