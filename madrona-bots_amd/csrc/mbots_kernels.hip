@@ -2556,6 +2556,9 @@ hipError_t launch_export_rows(const SimState &S, const ObsTable &nxt, int init, 
     else hipLaunchKernelGGL(export_rows_kernel<false>, dim3(world_blocks(S.W)), dim3(256), 0, st, S, nxt);
     return hipGetLastError();
 }
+#if defined(MB_PROBE_SHIFT) && !defined(MB_PROBE_BUILD)
+#error "MB_PROBE_SHIFT drops moves: a probe build (scripts/build_var.sh -DMB_PROBE_BUILD) only"
+#endif
 hipError_t launch_move(const SimState &S, const ObsTable &cur, const ObsTable &nxt, int prev_lazy,
                        int parts, hipStream_t st)
 {
@@ -2571,8 +2574,13 @@ hipError_t launch_move(const SimState &S, const ObsTable &cur, const ObsTable &n
         add(nxt.hidden, cur.hidden, 16, 4);
     } else if (parts & kMoveAHShift) {   // the fused shift: the Prev columns (the
                                         // current ones become their views)
+#ifdef MB_PROBE_SHIFT   // timing probes (wrong rows): 1 HiddenState only, 2/3 no A/H (3: no prev sensor either)
+        if (MB_PROBE_SHIFT == 1) add(nxt.phidden, cur.hidden, 16, 4);
+        if (MB_PROBE_SHIFT == 3) parts &= ~kMoveSensor;
+#else
         add(nxt.paction, cur.action, 8, 3);
         add(nxt.phidden, cur.hidden, 16, 4);
+#endif
     }
     if (parts & kMoveSensor) {
         add(nxt.psem, cur.sem, 16, 2);                   // prev sensor <- last step's sensor

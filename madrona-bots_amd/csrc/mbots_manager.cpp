@@ -112,7 +112,8 @@ struct mbots_handle {
     // last src_of when needed): PrevAction / PrevHiddenState, the six other
     // Prev* columns (from the other half's current ones when six_lazy)
     bool cur_ah_pending[2] = {false, false};   // Action / HiddenState themselves
-    bool psem_pending[2] = {false, false};     // the prev sensor (fused into the shift)
+    bool psem_pending[2] = {false, false};     // the prev sensor (moved only when read: dead at
+                                               // the next step)
     bool ah_pending[2] = {false, false};
     bool six_pending[2] = {false, false};
     bool six_lazy[2] = {false, false};
@@ -940,7 +941,9 @@ int mbots_step(mbots_handle *h, void *stream)
     if (h->six_pending[h->tb] && (rc = materialize_prev(h, st))) return rc;
     if ((rc = materialize_prev_ah(h, st))) return rc;
     if ((rc = materialize_cur_ah(h, st, 0))) return rc;
-    if ((rc = materialize_psem(h, st))) return rc;   // before this step's sensor rewrites its source
+    // (a prev sensor still owed is dead from here on: the new table's prev
+    // sensor is the last table's sensor rows, updateSensorOutputIdx
+    // sim.cpp:736-789, not its prev sensor -- so it is never moved)
     // K1 reads the learner's actions through the half's view (an aliased
     // Action column is its PrevAction), and so do this step's moves
     const mbots::ObsTable cur = src_view(h, h->tb);
@@ -1111,16 +1114,16 @@ int mbots_shift_observations(mbots_handle *h, void *stream)
     // shift).  Action / HiddenState still in the other half: one gather writes their
     // Prev copies, and the current columns become views of those (the learner
     // overwrites them next; DESIGN.md "Aliased current Action / HiddenState")
-    // -- the fused shift; the prev sensor rides along when still pending.
+    // -- the fused shift.  The step's prev-sensor move is not the shift's
+    // (shiftObservationsSystem, sim.cpp:1001-1035, leaves the sensor alone):
+    // it stays owed until a reader needs it and dies at the next step
+    // (DESIGN.md "Lazy prev sensor").
     const int tb = h->tb;
     const bool fused = h->cur_ah_pending[tb];
-    const bool with_psem = fused && h->psem_pending[tb];
     if (fused) {
         const mbots::ObsTable src = src_view(h, tb ^ 1);
-        if (with_psem && (rc = wait_prev_sensor(h, st))) return rc;   // the prev sensor's source rows
         rc = timed(h, MBOTS_TK_SHIFT, st, [&] {
-            return mbots::launch_move(h->S, src, h->T[tb], 0,
-                                      mbots::kMoveAHShift | (with_psem ? mbots::kMoveSensor : 0), st);
+            return mbots::launch_move(h->S, src, h->T[tb], 0, mbots::kMoveAHShift, st);
         });
     } else if (!(h->a_alias[tb] && h->h_alias[tb])) {   // both aliased: already equal
         if ((rc = materialize_cur_ah(h, st, 3))) return rc;
@@ -1133,7 +1136,6 @@ int mbots_shift_observations(mbots_handle *h, void *stream)
         h->prefetched &= mbots::kMoveSensor;
         if (fused) h->a_alias[tb] = h->h_alias[tb] = true;
         h->cur_ah_pending[tb] = false;
-        if (with_psem) h->psem_pending[tb] = false;
         h->prev_lazy[tb] = true;
         h->ah_pending[tb] = false;   // the shift wrote PrevAction / PrevHiddenState
         h->six_pending[tb] = false;  // ... and made the six the current columns
