@@ -366,14 +366,18 @@ def config5_loop(main_mgr, args, rank, world_size, dev, distributed):
     gsec = [0.0, 0.0]
     nrows = [0]
     gen = torch.Generator(device=dev).manual_seed(ACTION_SEED)
+    # slim learner records (128 B/agent instead of 272) from the second step
+    # on: rank 0 rebuilds Action / HiddenState / PrevHiddenState from its own
+    # last writes and the rows' provenance (harness/gather.py LearnerState)
+    state = None if args.full_records else gather.LearnerState()
 
     def one(t, timed):
         mgr.step()
         g0 = time.perf_counter()
         if distributed:
-            got, plan = gather.gather_learner(mgr, dst=0)
+            got, plan = gather.gather_learner(mgr, dst=0, state=state)
         else:   # one rank: the same records, packed and unpacked locally
-            got, plan = mb.unpack_learner(mgr.pack_learner()), None
+            got, plan = gather.gather_learner_local(mgr, state)
         actions = memory = None
         if got is not None:
             n = got["obs"].shape[0]
@@ -384,9 +388,11 @@ def config5_loop(main_mgr, args, rank, world_size, dev, distributed):
         g1 = time.perf_counter()
         mgr.shift_observations()
         if distributed:
-            gather.scatter_actions(mgr, actions, memory, plan, src=0)
+            gather.scatter_actions(mgr, actions, memory, plan, src=0, state=state)
         else:
             mgr.write_actions(actions, memory)
+            if state is not None:
+                state.commit(plan, actions, memory)
         if timed:
             gsec[0] += g1 - g0
             gsec[1] += time.perf_counter() - g1
@@ -409,22 +415,53 @@ def config5_loop(main_mgr, args, rank, world_size, dev, distributed):
         dist.barrier()
         dist.all_reduce(st, op=dist.ReduceOp.MAX)
     el, gs, ss = (float(x) for x in st.tolist())
-    rb = mgr.learner_record_bytes()
+    slim = state is not None and state.ready
+    rb = mgr.learner_record_bytes(slim)
+    # the learner rank's record work alone (untimed above: it overlaps the
+    # step there): pack + unpack (+ the rebuild from provenance) of one step's
+    # records on an idle device, priced at the bytes it must move per agent --
+    # pack reads the columns and writes the record (2 rb), unpack reads it (rb)
+    # and writes obs + prev_obs (2 x 276) + reward 4 + stats 16 (+ src 4); the
+    # rebuild gathers Action / HiddenState / PrevHiddenState (152 B read +
+    # written) -- and the xGMI payload per peer (every rank ships its records
+    # to rank 0 and receives 88 B of actions + memory per row)
+    rt = None
+    if not distributed:
+        mgr.step()
+        torch.cuda.synchronize()
+        r0 = time.perf_counter()
+        for _ in range(3):
+            got, _ = gather.gather_learner_local(mgr, state)
+            del got
+        torch.cuda.synchronize()
+        rt_ms = (time.perf_counter() - r0) / 3 * 1e3
+        n_rt = mgr.num_agents()
+        per = 3 * rb + 2 * 276 + 20 + (4 + 2 * 152 if slim else 0)
+        rt = {"ms": rt_ms, "rows": n_rt, "bytes_per_agent": per,
+              "achieved": n_rt * per / (rt_ms * 1e-3) / 1e9, "peak": 8000.0, "unit": "GB/s",
+              "frac": n_rt * per / (rt_ms * 1e-3) / 8e12,
+              "note": "pack + unpack (+ provenance rebuild) of one step's records on an idle device, host "
+                      "launch time included; bytes: 2 rb pack, rb + 572 (+ 4 src) unpack, 2 x 152 rebuild"}
+    rows_rank = mgr.num_agents()
     del mgr
     if rank != 0:
         return None
     rows = nrows[0] / steps
-    return {"what": "step + learner records (current and previous observation columns, reward, stats, Action, "
-                    f"HiddenState, PrevHiddenState: {rb} B/agent) gathered to rank 0 and unpacked there + "
-                    "actions / memory chosen there + shift + actions / memory scattered back to the owning ranks "
-                    "(harness/gather.py gather_learner / scatter_actions)",
+    return {"what": "step + what the learner reads (current and previous observation columns, reward, stats, "
+                    f"Action, HiddenState, PrevHiddenState; records of {rb} B/agent) gathered to rank 0 and "
+                    "unpacked there + actions / memory chosen there + shift + actions / memory scattered back to "
+                    "the owning ranks (harness/gather.py gather_learner / scatter_actions)",
             "backend": args.backend if distributed else "none (one rank: pack + unpack + write locally)",
             "n_gpus": world_size, "worlds_per_gpu": W5, "total_worlds": W5 * world_size,
             "steps": steps, "ms_per_step": el / steps * 1e3,
             "value": rows / (el / steps), "unit": "agent-steps/s (every rank's agents through the learner round trip)",
             "gather_ms_per_step": gs / steps * 1e3, "scatter_ms_per_step": ss / steps * 1e3,
             "rows_per_step_at_learner": rows,
-            "gathered_bytes_per_step": rows * rb, "scattered_bytes_per_step": rows * 88, "bytes_per_agent": rb}
+            "gathered_bytes_per_step": rows * rb, "scattered_bytes_per_step": rows * 88, "bytes_per_agent": rb,
+            "records": "slim: provenance, Action / HiddenState / PrevHiddenState rebuilt on rank 0" if slim
+                       else "full learner records",
+            "xgmi_bytes_per_step_per_peer": (rows_rank * rb + rows_rank * 88) if world_size > 1 else 0,
+            "roundtrip_roofline": rt}
 
 
 def main():
@@ -441,6 +478,8 @@ def main():
     ap.add_argument("--span-every", type=int, default=8,
                     help="bracket every k-th timed step()+shift() with HIP events (roofline "
                          "launch duration); each event pair adds ~10 us of GPU idle")
+    ap.add_argument("--full-records", action="store_true",
+                    help="config 5: ship the full 272-B learner records every step (no provenance rebuild)")
     ap.add_argument("--gather", action="store_true",
                     help="config 5 also at one rank (always run with several ranks): learner records "
                          "gathered to rank 0, actions / memory scattered back")

@@ -233,6 +233,30 @@ typedef struct mbots_learner_out {
 } mbots_learner_out;
 int mbots_unpack_learner(const void *records, uint64_t rows, int32_t with_depth, int32_t device,
                          const mbots_learner_out *out, void *stream);
+/* Slim learner records (config 5 with row provenance): the
+ * learner record without Action, HiddenState and PrevHiddenState -- 152 B of
+ * the 272 that only echo what the learner rank itself wrote (training_loop.py
+ * :136-137) one and two steps back, reordered by the species sort.  In their
+ * place the record carries each row's provenance: src, the row's index in the
+ * table before this step (-1: born or respawned this step), from which the
+ * learner rank rebuilds the three columns (harness/gather.py LearnerState):
+ *   bytes   0..59   as the learner record       60..63   src (int32)
+ *          64..115  as the learner record (the previous observation columns)
+ *         116..127  zero
+ *         128..191  depth, prev depth (uint8 x 32 each), only with
+ *                   MBOTS_FLAG_FIX_DEPTH_ALIAS
+ * The rebuilt columns equal the manager's as long as every row's Action and
+ * HiddenState were written after the last step and one or more shifts
+ * separate the two steps (the learner's loop).  mbots_pack_learner_slim
+ * moves none of the step's deferred columns: the previous observation rows
+ * the step still owes are gathered inside its launch. */
+#define MBOTS_LEARNER_SLIM_BYTES        128u
+#define MBOTS_LEARNER_SLIM_BYTES_DEPTH  192u
+int mbots_pack_learner_slim(mbots_handle *h, void *out, uint64_t out_rows, void *stream);
+/* records -> obs, prev_obs, reward, stats of `out` (its action / hidden /
+ * prev_hidden must be NULL) and src [rows] int32 (may be NULL) */
+int mbots_unpack_learner_slim(const void *records, uint64_t rows, int32_t with_depth, int32_t device,
+                              const mbots_learner_out *out, int32_t *src, void *stream);
 /* The learner's writes (training_loop.py:136-137: action_tensor[...] = one_hot,
  * memory_tensor[...] = new_memory) for every row at once: `rows` rows of
  * Action [rows, 6] int32 and/or HiddenState [rows, 16] f32 (either may be

@@ -100,6 +100,7 @@ Sim::Sim(const mbots_config &cfg)
     put(zeros_rows_, rows);
     put(zeros_worlds_, W_);
     put(sensor_index_, rows);
+    put(src_of_, rows);
     // Sim::Sim + initWorld (sim.cpp:1232-1256, :233-275), then the first export
     for_worlds([&](uint32_t w) { init_world(w); });
     scan();
@@ -417,6 +418,7 @@ void Sim::export_world(uint32_t w, const Table &cur, Table &nxt, bool init)
         mv(nxt.phidden, cur.phidden, r, o, kHidden);
         mv(nxt.psem, cur.sem, r, o, kSensor);
         if (fixd) mv(nxt.pdepth, cur.depth, r, o, kSensor);
+        src_of_[r] = o;
         obsrow_[s] = (int32_t)r;
     }
 }

@@ -45,6 +45,9 @@ public:
     uint64_t agent_steps() const { return agent_steps_; }
     uint64_t overflow() const;
     Table &table() { return T_[tb_]; }
+    // each export row's row in the table before the last step (-1: new), like
+    // the HIP path's src_of (slim learner records)
+    const int32_t *src_of() const { return src_of_.data(); }
     void world_state(uint32_t w, float *xy_rwrz, int32_t *sp_hp_finder, uint64_t *food,
                      uint32_t *food_rot, int32_t *n_out) const;
     uint64_t checkpoint_bytes() const;
@@ -78,7 +81,7 @@ private:
     uint32_t N_ = 0;
     uint32_t totals_[5] = {};
     uint64_t agent_steps_ = 0;
-    std::vector<int32_t> zeros_rows_, zeros_worlds_, sensor_index_;
+    std::vector<int32_t> zeros_rows_, zeros_worlds_, sensor_index_, src_of_;
 };
 
 }  // namespace cpu

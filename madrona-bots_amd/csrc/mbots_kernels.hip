@@ -2245,16 +2245,92 @@ __global__ __launch_bounds__(256) void pack_learner_kernel(const uint32_t *total
     }
 }
 
+// Slim learner records (include/mbots.h MBOTS_LEARNER_SLIM_BYTES): the learner
+// record's observation part plus each row's provenance src_of[r] at byte 60;
+// no Action / HiddenState / PrevHiddenState (the learner rank rebuilds them
+// from its own writes, harness/gather.py).  The previous observation columns
+// a step still owes (its deferred Prev moves, the lazy prev sensor) are
+// gathered here along src_of from the last table -- what the move would write,
+// zero for a newborn -- so a pack after step() launches nothing else.
+struct LearnerSlimCols {
+    const int8_t *sem;
+    const uint8_t *depth;
+    const int32_t *health, *stats, *src_of;
+    const float *pos, *sur, *reward;
+    const int8_t *psem;         // prev sensor: rows r, or old rows (gsem)
+    const uint8_t *pdepth;
+    const int32_t *phealth;     // prev health / position / surrounding: rows r, or old rows (g6)
+    const float *ppos, *psur;
+    int gsem, g6;
+};
+
+__global__ __launch_bounds__(256) void pack_learner_slim_kernel(const uint32_t *totals, LearnerSlimCols c, int fixd,
+                                                                uint8_t *out, uint32_t out_rows)
+{
+    const uint32_t N = min(totals[0], out_rows);
+    const uint32_t rec = fixd ? kLearnerSlimBytesDepth : kLearnerSlimBytes;
+    for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r < N; r += gridDim.x * blockDim.x) {
+        uint4 *o = reinterpret_cast<uint4 *>(out + (size_t)r * rec);
+        const int32_t src = c.src_of[r];
+        const uint4 *s = reinterpret_cast<const uint4 *>(c.sem + (size_t)r * kSensor);
+        o[0] = s[0];
+        o[1] = s[1];
+        const float2 p = reinterpret_cast<const float2 *>(c.pos)[r];
+        const float2 su = reinterpret_cast<const float2 *>(c.sur)[r];
+        const int4 st = reinterpret_cast<const int4 *>(c.stats)[r];
+        const uint32_t sb = (uint32_t)(st.x & 0xFF) | (uint32_t)(st.y & 0xFF) << 8 |
+                            (uint32_t)(st.z & 0xFF) << 16 | (uint32_t)(st.w & 0xFF) << 24;
+        o[2] = make_uint4((uint32_t)c.health[r], __float_as_uint(p.x), __float_as_uint(p.y), __float_as_uint(su.x));
+        o[3] = make_uint4(__float_as_uint(su.y), __float_as_uint(c.reward[r]), sb, (uint32_t)src);
+        // the previous columns: this row's, or its old row's in the last table
+        const int32_t ps = c.gsem ? src : (int32_t)r, p6 = c.g6 ? src : (int32_t)r;
+        uint4 a = make_uint4(0u, 0u, 0u, 0u), b = a;
+        if (ps >= 0) {
+            a = reinterpret_cast<const uint4 *>(c.psem + (size_t)ps * kSensor)[0];
+            b = reinterpret_cast<const uint4 *>(c.psem + (size_t)ps * kSensor)[1];
+        }
+        o[4] = a;
+        o[5] = b;
+        uint32_t ph = 0u;
+        float2 pp = make_float2(0.0f, 0.0f), psu = pp;
+        if (p6 >= 0) {
+            ph = (uint32_t)c.phealth[p6];
+            pp = reinterpret_cast<const float2 *>(c.ppos)[p6];
+            psu = reinterpret_cast<const float2 *>(c.psur)[p6];
+        }
+        o[6] = make_uint4(ph, __float_as_uint(pp.x), __float_as_uint(pp.y), __float_as_uint(psu.x));
+        o[7] = make_uint4(__float_as_uint(psu.y), 0u, 0u, 0u);
+        if (fixd) {
+            const uint4 *d = reinterpret_cast<const uint4 *>(c.depth + (size_t)r * kSensor);
+            o[8] = d[0];
+            o[9] = d[1];
+            uint4 e = make_uint4(0u, 0u, 0u, 0u), f = e;
+            if (ps >= 0) {
+                e = reinterpret_cast<const uint4 *>(c.pdepth + (size_t)ps * kSensor)[0];
+                f = reinterpret_cast<const uint4 *>(c.pdepth + (size_t)ps * kSensor)[1];
+            }
+            o[10] = e;
+            o[11] = f;
+        }
+    }
+}
+
 // Learner side: records -> obs / prev_obs [N, 69] (construct_obs of the
 // current / previous columns, bit-identical), reward [N], stats [N, 4],
 // action [N, 6], hidden / prev_hidden [N, 16]; any output but obs may be null.
 // 64 records per block staged in LDS, every output written as contiguous runs.
+// (slim: the slim records -- depth at 128 / 160 -- and src [N] instead of
+// action / hidden / prev_hidden)
 __global__ __launch_bounds__(256) void unpack_learner_kernel(const uint8_t *recs, uint32_t N, int fixd,
-                                                             mbots_learner_out o)
+                                                             mbots_learner_out o, int slim, int32_t *src)
 {
     constexpr int kW = kLearnerBytesDepth / 16;   // granules per staged record (the widest)
     __shared__ uint4 s_rec[kObsRows * kW];
-    const uint32_t rec = fixd ? kLearnerBytesDepth : kLearnerBytes, gpr = rec / 16;
+    const uint32_t rec = slim ? (fixd ? kLearnerSlimBytesDepth : kLearnerSlimBytes)
+                              : (fixd ? kLearnerBytesDepth : kLearnerBytes),
+                   gpr = rec / 16;
+    // depth bytes: current at dc, previous at 64 + dp
+    const uint32_t dc = slim ? 128u : 272u, dp = slim ? 96u : 240u;
     const uint32_t nblk = (N + kObsRows - 1) / kObsRows;
     const uint32_t t = threadIdx.x;
     const uint8_t *sb = reinterpret_cast<const uint8_t *>(s_rec);
@@ -2263,7 +2339,7 @@ __global__ __launch_bounds__(256) void unpack_learner_kernel(const uint8_t *recs
         const uint32_t r = i / kObsDim, c = i - r * kObsDim;
         const uint8_t *q = sb + (size_t)r * kW * 16 + (prev ? 64 : 0);
         const uint32_t *q32 = reinterpret_cast<const uint32_t *>(q);
-        if (c < 32) return (float)q[fixd ? (prev ? 240 : 272) + c : c];
+        if (c < 32) return (float)q[fixd ? (prev ? dp : dc) + c : c];
         if (c < 35) return __uint_as_float(q32[8 + (c - 32)]);
         if (c < 67) return (float)(int8_t)q[c - 35];
         return __uint_as_float(q32[11 + (c - 67)]);
@@ -2302,6 +2378,7 @@ __global__ __launch_bounds__(256) void unpack_learner_kernel(const uint8_t *recs
             o.stats[4 * (size_t)(r0 + t) + 2] = (int32_t)((s4 >> 16) & 0xFF);
             o.stats[4 * (size_t)(r0 + t) + 3] = (int32_t)(s4 >> 24);
         }
+        if (src && t < nr) src[r0 + t] = (int32_t)word(t, 60);
         if (o.action)
             for (uint32_t i = t; i < nr * 6; i += 256) {
                 const uint32_t r = i / 6, k = i - r * 6;
@@ -2751,7 +2828,50 @@ hipError_t launch_unpack_learner(const void *recs, uint32_t n, int fixd, const m
     if (n == 0) return hipSuccess;
     const unsigned blocks = (unsigned)std::min<uint64_t>((n + kObsRows - 1) / kObsRows, 16384);
     hipLaunchKernelGGL(unpack_learner_kernel, dim3(blocks), dim3(256), 0, st, static_cast<const uint8_t *>(recs), n,
-                       fixd, o);
+                       fixd, o, 0, (int32_t *)nullptr);
+    return hipGetLastError();
+}
+hipError_t launch_pack_learner_slim(const SimState &S, const ObsTable &t, int prev_lazy, const ObsTable *six_src,
+                                    int six_lazy, const ObsTable *sem_src, void *out, uint32_t out_rows,
+                                    hipStream_t st)
+{
+    const int fixd = (S.flags & kFlagFixDepth) != 0;
+    LearnerSlimCols c;
+    c.sem = t.sem;
+    c.depth = t.depth;
+    c.health = t.health;
+    c.stats = t.stats;
+    c.src_of = S.src_of;
+    c.pos = t.pos;
+    c.sur = t.sur;
+    c.reward = t.reward;
+    c.gsem = sem_src != nullptr;
+    c.psem = sem_src ? sem_src->sem : t.psem;
+    c.pdepth = sem_src ? sem_src->depth : t.pdepth;
+    c.g6 = six_src != nullptr;
+    if (six_src) {
+        const bool lz = six_lazy != 0;
+        c.phealth = lz ? six_src->health : six_src->phealth;
+        c.ppos = lz ? six_src->pos : six_src->ppos;
+        c.psur = lz ? six_src->sur : six_src->psur;
+    } else {
+        const bool lz = prev_lazy != 0;
+        c.phealth = lz ? t.health : t.phealth;
+        c.ppos = lz ? t.pos : t.ppos;
+        c.psur = lz ? t.sur : t.psur;
+    }
+    const unsigned blocks = (unsigned)std::min<uint64_t>((out_rows + 255) / 256, 8192);
+    hipLaunchKernelGGL(pack_learner_slim_kernel, dim3(std::max(blocks, 1u)), dim3(256), 0, st, S.totals, c, fixd,
+                       static_cast<uint8_t *>(out), out_rows);
+    return hipGetLastError();
+}
+hipError_t launch_unpack_learner_slim(const void *recs, uint32_t n, int fixd, const mbots_learner_out &o,
+                                      int32_t *src, hipStream_t st)
+{
+    if (n == 0) return hipSuccess;
+    const unsigned blocks = (unsigned)std::min<uint64_t>((n + kObsRows - 1) / kObsRows, 16384);
+    hipLaunchKernelGGL(unpack_learner_kernel, dim3(blocks), dim3(256), 0, st, static_cast<const uint8_t *>(recs), n,
+                       fixd, o, 1, src);
     return hipGetLastError();
 }
 hipError_t launch_sensor_index(const SimState &S, int32_t *out, hipStream_t st)

@@ -146,5 +146,16 @@ hipError_t launch_pack_learner(const SimState &S, const ObsTable &t, int prev_la
                                hipStream_t st);
 hipError_t launch_unpack_learner(const void *recs, uint32_t n, int fixd, const mbots_learner_out &o,
                                  hipStream_t st);
+// slim learner records (MBOTS_LEARNER_SLIM_BYTES[_DEPTH]): `t` the current half
+// (prev_lazy: its six Prev* columns are the current ones); the previous
+// observation columns the step still owes are gathered along S.src_of inside
+// the launch -- the six from `six_src` (six_lazy: from its current columns),
+// the prev sensor from `sem_src`'s sensor rows -- when those are non-null
+constexpr uint32_t kLearnerSlimBytes = 128, kLearnerSlimBytesDepth = 192;
+hipError_t launch_pack_learner_slim(const SimState &S, const ObsTable &t, int prev_lazy, const ObsTable *six_src,
+                                    int six_lazy, const ObsTable *sem_src, void *out, uint32_t out_rows,
+                                    hipStream_t st);
+hipError_t launch_unpack_learner_slim(const void *recs, uint32_t n, int fixd, const mbots_learner_out &o,
+                                      int32_t *src, hipStream_t st);
 
 }  // namespace mbots

@@ -690,17 +690,43 @@ void pack_learner_host(const mbots::cpu::Table &t, bool fixd, uint64_t n, uint8_
     }
 }
 
-void unpack_learner_host(const uint8_t *recs, uint64_t n, bool fixd, const mbots_learner_out &o)
+// slim learner records on the host (CPU mode: every column materialised)
+void pack_learner_slim_host(const mbots::cpu::Table &t, const int32_t *src_of, bool fixd, uint64_t n,
+                            uint8_t *out)
 {
-    const size_t rec = fixd ? MBOTS_LEARNER_BYTES_DEPTH : MBOTS_LEARNER_BYTES;
+    const size_t rec = fixd ? MBOTS_LEARNER_SLIM_BYTES_DEPTH : MBOTS_LEARNER_SLIM_BYTES;
+    for (uint64_t r = 0; r < n; ++r) {
+        uint8_t *o = out + r * rec;
+        pack_rollout_host(t.sem.data() + r * mbots::kSensor, nullptr, t.health.data() + r, t.pos.data() + 2 * r,
+                          t.sur.data() + 2 * r, t.reward.data() + r, t.stats.data() + 4 * r, 1, o);
+        memcpy(o + 60, src_of + r, 4);
+        memcpy(o + 64, t.psem.data() + r * mbots::kSensor, 32);
+        memcpy(o + 96, t.phealth.data() + r, 4);
+        memcpy(o + 100, t.ppos.data() + 2 * r, 8);
+        memcpy(o + 108, t.psur.data() + 2 * r, 8);
+        memset(o + 116, 0, 12);
+        if (fixd) {
+            memcpy(o + 128, t.depth.data() + r * mbots::kSensor, 32);
+            memcpy(o + 160, t.pdepth.data() + r * mbots::kSensor, 32);
+        }
+    }
+}
+
+void unpack_learner_host(const uint8_t *recs, uint64_t n, bool fixd, const mbots_learner_out &o, bool slim = false,
+                         int32_t *src = nullptr)
+{
+    const size_t rec = slim ? (fixd ? MBOTS_LEARNER_SLIM_BYTES_DEPTH : MBOTS_LEARNER_SLIM_BYTES)
+                            : (fixd ? MBOTS_LEARNER_BYTES_DEPTH : MBOTS_LEARNER_BYTES);
+    const size_t dc = slim ? 128 : 272, dp = slim ? 160 : 304;
     for (uint64_t r = 0; r < n; ++r) {
         const uint8_t *q = recs + r * rec;
+        if (src) memcpy(src + r, q + 60, 4);
         for (int prev = 0; prev < 2; ++prev) {
             float *ob = prev ? o.prev_obs : o.obs;
             if (!ob) continue;
             ob += r * 69;
             const uint8_t *b = q + (prev ? 64 : 0);
-            const uint8_t *d = fixd ? q + (prev ? 304 : 272) : b;
+            const uint8_t *d = fixd ? q + (prev ? dp : dc) : b;
             for (int c = 0; c < 32; ++c) ob[c] = (float)d[c];
             memcpy(ob + 32, b + 32, 12);   // health bits, position
             for (int c = 0; c < 32; ++c) ob[35 + c] = (float)(int8_t)b[c];
@@ -709,6 +735,7 @@ void unpack_learner_host(const uint8_t *recs, uint64_t n, bool fixd, const mbots
         if (o.reward) memcpy(o.reward + r, q + 52, 4);
         if (o.stats)
             for (int k = 0; k < 4; ++k) o.stats[4 * r + k] = q[56 + k];
+        if (slim) continue;
         if (o.action) memcpy(o.action + 6 * r, q + 116, 24);
         if (o.hidden) memcpy(o.hidden + mbots::kHidden * r, q + 144, 64);
         if (o.prev_hidden) memcpy(o.prev_hidden + mbots::kHidden * r, q + 208, 64);
@@ -1421,6 +1448,53 @@ int mbots_pack_learner(mbots_handle *h, void *out, uint64_t out_rows, void *stre
         return mbots::launch_pack_learner(h->S, h->T[h->tb], h->prev_lazy[h->tb] ? 1 : 0, out, (uint32_t)out_rows,
                                           st);
     });
+}
+
+int mbots_pack_learner_slim(mbots_handle *h, void *out, uint64_t out_rows, void *stream)
+{
+    if (!h || !out) return fail(MBOTS_E_INVALID, "null argument");
+    if (out_rows > 0xFFFFFFFFull) return fail(MBOTS_E_INVALID, "out_rows too large");
+    const bool fixd = (h->cfg.flags & MBOTS_FLAG_FIX_DEPTH_ALIAS) != 0;
+    if (h->cpu) {
+        pack_learner_slim_host(h->cpu->table(), h->cpu->src_of(), fixd,
+                               std::min<uint64_t>(h->cpu->num_agents(), out_rows), static_cast<uint8_t *>(out));
+        return MBOTS_OK;
+    }
+    if ((reinterpret_cast<uintptr_t>(out) & 15u) != 0) return fail(MBOTS_E_INVALID, "out must be 16-byte aligned");
+    HIP_TRY(hipSetDevice(h->device));
+    hipStream_t st = as_stream(stream);
+    int rc = use_stream(h, st);
+    if (rc) return rc;
+    // the sensor rows (and in K1-finder mode the prev sensor rows it moved);
+    // in the joined schedule the last sensor's rows, the source of a prev
+    // sensor still owed, were waited for by this step's K1
+    if ((rc = wait_sensor(h, st))) return rc;
+    const int tb = h->tb;
+    const mbots::ObsTable &last = h->T[tb ^ 1];
+    return timed(h, MBOTS_TK_OBS, st, [&] {
+        return mbots::launch_pack_learner_slim(h->S, h->T[tb], h->prev_lazy[tb] ? 1 : 0,
+                                               h->six_pending[tb] ? &last : nullptr, h->six_lazy[tb] ? 1 : 0,
+                                               h->psem_pending[tb] ? &last : nullptr, out, (uint32_t)out_rows, st);
+    });
+}
+
+int mbots_unpack_learner_slim(const void *records, uint64_t rows, int32_t with_depth, int32_t device,
+                              const mbots_learner_out *out, int32_t *src, void *stream)
+{
+    if (!out || (!records && rows)) return fail(MBOTS_E_INVALID, "null argument");
+    if (out->action || out->hidden || out->prev_hidden)
+        return fail(MBOTS_E_INVALID, "slim records carry no Action / HiddenState / PrevHiddenState");
+    if (rows > 0xFFFFFFFFull) return fail(MBOTS_E_INVALID, "rows too large");
+    if (device < 0) {
+        unpack_learner_host(static_cast<const uint8_t *>(records), rows, with_depth != 0, *out, true, src);
+        return MBOTS_OK;
+    }
+    if ((reinterpret_cast<uintptr_t>(records) & 15u) != 0)
+        return fail(MBOTS_E_INVALID, "records must be 16-byte aligned");
+    HIP_TRY(hipSetDevice(device));
+    HIP_TRY(mbots::launch_unpack_learner_slim(records, (uint32_t)rows, with_depth ? 1 : 0, *out, src,
+                                              as_stream(stream)));
+    return MBOTS_OK;
 }
 
 int mbots_unpack_learner(const void *records, uint64_t rows, int32_t with_depth, int32_t device,

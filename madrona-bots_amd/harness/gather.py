@@ -105,14 +105,16 @@ def exchange_plan(mgr, group=None):
     return {"counts": allc[:, :4], "first": allc[:, 4:]}
 
 
-def gather_learner(mgr, dst=0, group=None, keys=None):
+def gather_learner(mgr, dst=0, group=None, keys=None, state=None):
     """Config 5, learner side of the step: every rank packs its export rows'
     learner records (SimManager.pack_learner: current and previous observation
     columns, reward, stats, Action, HiddenState, PrevHiddenState -- what
     learn/training_loop.py:43-93 reads), one padded gather ships them to `dst`,
     which reassembles the global (species, world, slot) order and unpacks them
     (madrona_bots.unpack_learner).  Returns (tensors on `dst` / None elsewhere,
-    plan) -- the plan is scatter_actions' argument."""
+    plan) -- the plan is scatter_actions' argument.  With a ready
+    LearnerState the ranks ship slim records (128 B instead of 272) and `dst`
+    rebuilds Action / HiddenState / PrevHiddenState from its own last writes."""
     import madrona_bots as mb
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
@@ -122,17 +124,130 @@ def gather_learner(mgr, dst=0, group=None, keys=None):
     plan = exchange_plan(mgr, group)
     all_cnt = plan["counts"]
     n_max = int(all_cnt.sum(dim=1).max())
-    rb = mgr.learner_record_bytes()
+    slim = state is not None and state.ready
+    rb = mgr.learner_record_bytes(slim)
     pad = torch.empty((max(n_max, 1), rb), dtype=torch.uint8, device=dev)   # rows past N: padding
-    mgr.pack_learner(pad)
+    mgr.pack_learner(pad, slim=slim)
     send = pad if cdev.type == dev.type else pad.to(cdev)
     bufs = [torch.empty_like(send) for _ in range(world)] if rank == dst else None
     dist.gather(send, bufs, dst=dst_global, group=group)
     if rank != dst:
         return None, plan
     recs = reassemble([b[:n_max] for b in bufs], all_cnt)
-    kw = {} if keys is None else {"keys": keys}
-    return mb.unpack_learner(recs.to(dev), **kw), plan
+    if slim:
+        got = rebuild(mb.unpack_learner(recs.to(dev)), row_ranks(all_cnt), state)
+    else:   # (the state keeps this step's HiddenState: every key then)
+        kw = {} if keys is None or state is not None else {"keys": keys}
+        got = mb.unpack_learner(recs.to(dev), **kw)
+    if state is not None:
+        state.note_gathered(got)
+    if keys is not None:
+        got = {k: got[k] for k in keys}
+    return got, plan
+
+
+class LearnerState:
+    """What the learner rank remembers of its own writes, so the ranks can
+    ship slim learner records (include/mbots.h MBOTS_LEARNER_SLIM_BYTES: no
+    Action, HiddenState, PrevHiddenState -- 152 of the 272 B per agent -- but
+    each row's provenance src, its index in the table before the step).  After
+    step t the manager's columns are the learner's own values moved by the
+    species sort (learn/training_loop.py:136-137 wrote them after step t-1;
+    the shift copied HiddenState into PrevHiddenState first):
+
+        Action(t)[r]          = A_{t-1}[src[r]]
+        HiddenState(t)[r]     = M_{t-1}[src[r]]
+        PrevHiddenState(t)[r] = HiddenState(t-1)[src[r]]     (0 for src = -1)
+
+    with A_{t-1} / M_{t-1} the actions and memory scattered after step t-1 and
+    src mapped from the owning rank's old rows into the last global table
+    (that step's plan).  Valid while every row's action and memory are written
+    after every step (scatter_actions does) -- after any other write, a
+    checkpoint load or a new manager, call reset() on every rank: the next
+    gather then ships full records again.  Every rank holds one (they agree on
+    the record width); only the learner rank holds tensors.  The learner must
+    not modify the actions / memory it passed to scatter_actions in place."""
+
+    def __init__(self):
+        self.reset()
+
+    def reset(self):
+        self.ready = False
+        self.counts = None            # [ranks, 4] per-rank species rows of the last table
+        self.action = self.memory = self.hidden = None   # its rows, global order
+        self._hidden_now = None       # HiddenState of the table being learned on
+
+    def note_gathered(self, got):
+        if got is not None:
+            self._hidden_now = got["hidden"]
+
+    def commit(self, plan, actions, memory):
+        """After the learner's writes went out (every rank)."""
+        if actions is not None:
+            self.counts = plan["counts"].clone()
+            self.action, self.memory, self.hidden = actions, memory, self._hidden_now
+        self._hidden_now = None
+        self.ready = True
+
+
+def row_ranks(counts):
+    """The owning rank of every row of the global (species, world, slot) order
+    reassemble() builds from per-rank species counts [ranks, 4]."""
+    ranks = counts.shape[0]
+    ids = torch.arange(ranks).repeat(4)
+    return torch.repeat_interleave(ids, counts.t().reshape(-1).to(torch.int64))
+
+
+def provenance_rows(src, owner, last_counts):
+    """Global row of each row's old row in the last table: src [N] int32 (the
+    owning rank's local old row, -1 new), owner [N] its rank, last_counts
+    [ranks, 4] the last table's per-rank species rows.  Returns int64 [N]
+    (-1 for new rows)."""
+    dev = src.device
+    lc = last_counts.to(device=dev, dtype=torch.int64)
+    lstart = torch.cumsum(lc, dim=1) - lc                       # [R, 4] local species starts
+    tot = lc.sum(dim=0)
+    gstart = (torch.cumsum(tot, 0) - tot)[None, :] + (torch.cumsum(lc, dim=0) - lc)   # [R, 4]
+    o = src.to(torch.int64)
+    valid = o >= 0
+    oc = o.clamp(min=0)
+    ls = lstart[owner.to(dev)]                                  # [N, 4]
+    sp = ((oc[:, None] >= ls).sum(dim=1) - 1).clamp(min=0)      # the old row's species segment
+    g = gstart[owner.to(dev), sp] + oc - ls.gather(1, sp[:, None]).squeeze(1)
+    return torch.where(valid, g, torch.full_like(g, -1))
+
+
+def rebuild(got, owner, state):
+    """Slim records: Action / HiddenState / PrevHiddenState of every gathered
+    row from the learner's own last writes (LearnerState), bit-identical to
+    the manager's columns."""
+    g = provenance_rows(got["src"], owner, state.counts)
+    valid = (g >= 0)[:, None]
+    gi = g.clamp(min=0)
+
+    def take(t):
+        if t.shape[0] == 0:
+            return torch.zeros((g.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=g.device)
+        return torch.where(valid, t.index_select(0, gi), torch.zeros((), dtype=t.dtype, device=t.device))
+    got["action"] = take(state.action.to(torch.int32))
+    got["hidden"] = take(state.memory.to(torch.float32))
+    got["prev_hidden"] = take(state.hidden)
+    return got
+
+
+def gather_learner_local(mgr, state=None):
+    """gather_learner for one rank without torch.distributed: the same records
+    packed and unpacked locally (slim ones once `state` is ready)."""
+    import madrona_bots as mb
+    counts = mgr.species_count_tensor().to_torch()
+    plan = {"counts": counts.sum(dim=0).to(torch.int64).cpu()[None], "first": counts[0].to(torch.int64).cpu()[None]}
+    slim = state is not None and state.ready
+    got = mb.unpack_learner(mgr.pack_learner(slim=slim))
+    if slim:
+        got = rebuild(got, torch.zeros(got["src"].shape[0], dtype=torch.int64, device=got["src"].device), state)
+    if state is not None:
+        state.note_gathered(got)
+    return got, plan
 
 
 def split_rows(glob, plan, r):
@@ -155,12 +270,13 @@ def split_rows(glob, plan, r):
     return torch.cat(parts)
 
 
-def scatter_actions(mgr, actions, memory, plan, src=0, group=None):
+def scatter_actions(mgr, actions, memory, plan, src=0, group=None, state=None):
     """The learner's writes (training_loop.py:136-137) sent to the ranks that
     own the rows: on `src`, int32 [sum N_r, 6] actions and
     float32 [sum N_r, 16] memory in the global order gather_learner produced;
     every rank receives its rows (plus its shard ghost's) in one padded
-    scatter and writes them with SimManager.write_actions."""
+    scatter and writes them with SimManager.write_actions.  `state`: the
+    LearnerState the next gather_learner rebuilds from (every rank)."""
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
     src_global = src if group is None else dist.get_global_rank(group, src)
@@ -185,6 +301,8 @@ def scatter_actions(mgr, actions, memory, plan, src=0, group=None):
         raise RuntimeError(f"rank {rank}: {mine.shape[0]} rows received, the table holds {mgr.num_rows()} "
                            "(is shard_ghost set on every rank but the last?)")
     mgr.write_actions(mine[:, :6].contiguous(), mine[:, 6:].contiguous().view(torch.float32))
+    if state is not None:
+        state.commit(plan, actions if rank == src else None, memory if rank == src else None)
 
 
 def gather_rollout(tensors, rows_per_species, dst=0, group=None):

@@ -83,6 +83,8 @@ def _load():
         "mbots_learner_record_bytes": [vp, P(u32)],
         "mbots_pack_learner": [vp, vp, ctypes.c_uint64, vp],
         "mbots_unpack_learner": [vp, ctypes.c_uint64, i32, i32, P(_LearnerOut), vp],
+        "mbots_pack_learner_slim": [vp, vp, ctypes.c_uint64, vp],
+        "mbots_unpack_learner_slim": [vp, ctypes.c_uint64, i32, i32, P(_LearnerOut), vp, vp],
         "mbots_write_actions": [vp, vp, vp, ctypes.c_uint64, vp],
         "mbots_num_rows": [vp, P(u32)],
         "mbots_agent_steps": [vp, P(ctypes.c_uint64)],
@@ -273,34 +275,52 @@ def unpack_rollout(records, with_depth=None):
 
 
 LEARNER_BYTES, LEARNER_BYTES_DEPTH = 272, 336
+LEARNER_SLIM_BYTES, LEARNER_SLIM_BYTES_DEPTH = 128, 192
 _LEARNER_KEYS = ("obs", "prev_obs", "reward", "stats", "action", "hidden", "prev_hidden")
+_SLIM_KEYS = ("obs", "prev_obs", "reward", "stats", "src")
 
 
-def unpack_learner(records, with_depth=None, keys=_LEARNER_KEYS):
+def unpack_learner(records, with_depth=None, keys=None):
     """Learner side of the config-5 round trip: uint8 [N, 272 | 336] learner
     records (SimManager.pack_learner, gathered from every rank) -> the columns
     learn/training_loop.py reads after step(): "obs" / "prev_obs" float32
     [N, 69] (construct_obs of the current / previous columns, bit-identical),
     "reward" [N, 1], "stats" int32 [N, 4], "action" int32 [N, 6], "hidden" /
     "prev_hidden" float32 [N, 16] (mbots_unpack_learner), on the records'
-    device; `keys` selects the outputs."""
-    if records.dtype != torch.uint8 or records.dim() != 2 or \
-            records.shape[1] not in (LEARNER_BYTES, LEARNER_BYTES_DEPTH):
-        raise ValueError(f"records must be uint8 [N, {LEARNER_BYTES}] or [N, {LEARNER_BYTES_DEPTH}]")
-    depth = records.shape[1] == LEARNER_BYTES_DEPTH if with_depth is None else bool(with_depth)
-    if depth != (records.shape[1] == LEARNER_BYTES_DEPTH):
+    device; `keys` selects the outputs.  Slim records (uint8 [N, 128 | 192],
+    SimManager.pack_learner(slim=True)) give "obs", "prev_obs", "reward",
+    "stats" and "src" int32 [N] -- each row's index in the table before the
+    step, -1 for a newborn (mbots_unpack_learner_slim; harness/gather.py
+    rebuilds action / hidden / prev_hidden from it)."""
+    widths = (LEARNER_BYTES, LEARNER_BYTES_DEPTH, LEARNER_SLIM_BYTES, LEARNER_SLIM_BYTES_DEPTH)
+    if records.dtype != torch.uint8 or records.dim() != 2 or records.shape[1] not in widths:
+        raise ValueError(f"records must be uint8 [N, w], w in {widths}")
+    slim = records.shape[1] in (LEARNER_SLIM_BYTES, LEARNER_SLIM_BYTES_DEPTH)
+    wide = LEARNER_SLIM_BYTES_DEPTH if slim else LEARNER_BYTES_DEPTH
+    depth = records.shape[1] == wide if with_depth is None else bool(with_depth)
+    if depth != (records.shape[1] == wide):
         raise ValueError("with_depth does not match the record width")
+    keys = (_SLIM_KEYS if slim else _LEARNER_KEYS) if keys is None else tuple(keys)
+    allowed = _SLIM_KEYS if slim else _LEARNER_KEYS
+    if any(k not in allowed for k in keys):
+        raise ValueError(f"keys must be among {allowed}")
     rec = records.contiguous()
     n, dev = rec.shape[0], rec.device
     shapes = {"obs": ((n, OBS_DIM), torch.float32), "prev_obs": ((n, OBS_DIM), torch.float32),
               "reward": ((n, 1), torch.float32), "stats": ((n, 4), torch.int32),
               "action": ((n, 6), torch.int32), "hidden": ((n, 16), torch.float32),
-              "prev_hidden": ((n, 16), torch.float32)}
+              "prev_hidden": ((n, 16), torch.float32), "src": ((n,), torch.int32)}
     out = {k: torch.empty(shapes[k][0], dtype=shapes[k][1], device=dev) for k in keys}
     lo = _LearnerOut(**{k: (out[k].data_ptr() if k in out else None) for k in _LEARNER_KEYS})
     stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream if dev.type == "cuda" else None)
-    _check(_lib.mbots_unpack_learner(ctypes.c_void_p(rec.data_ptr()), n, 1 if depth else 0,
-                                     dev.index if dev.type == "cuda" else -1, ctypes.byref(lo), stream))
+    devi = dev.index if dev.type == "cuda" else -1
+    if slim:
+        src = ctypes.c_void_p(out["src"].data_ptr() if "src" in out else None)
+        _check(_lib.mbots_unpack_learner_slim(ctypes.c_void_p(rec.data_ptr()), n, 1 if depth else 0, devi,
+                                              ctypes.byref(lo), src, stream))
+    else:
+        _check(_lib.mbots_unpack_learner(ctypes.c_void_p(rec.data_ptr()), n, 1 if depth else 0, devi,
+                                         ctypes.byref(lo), stream))
     return out
 
 
@@ -343,6 +363,7 @@ class SimManager:
         self._h = h
         # row slots of every table column (the shard ghost is one more world)
         self._cap_rows = (self.num_worlds + (1 if shard_ghost else 0)) * self.agent_capacity
+        self._fix_depth = bool(fix_depth_alias)
         self._views = {}
 
     def _stream(self):
@@ -502,28 +523,34 @@ class SimManager:
         _check(_lib.mbots_num_rows(self._h, ctypes.byref(v)))
         return v.value
 
-    def learner_record_bytes(self):
-        """Bytes per learner record (include/mbots.h: 272, or 336 with real depth)."""
+    def learner_record_bytes(self, slim=False):
+        """Bytes per learner record (include/mbots.h: 272, or 336 with real
+        depth; slim records 128 / 192)."""
+        if slim:
+            return LEARNER_SLIM_BYTES_DEPTH if self._fix_depth else LEARNER_SLIM_BYTES
         v = ctypes.c_uint32()
         _check(_lib.mbots_learner_record_bytes(self._h, ctypes.byref(v)))
         return v.value
 
-    def pack_learner(self, out=None):
+    def pack_learner(self, out=None, slim=False):
         """Everything the reference training loop reads after step() --
         current and previous observation columns, reward, stats, Action,
         HiddenState, PrevHiddenState (learn/training_loop.py:43-93) -- as one
         uint8 [N, learner_record_bytes()] record per export row: the payload of
         the config-5 gather (harness/gather.py); unpack_learner() rebuilds the
-        learner's tensors.  `out` may hold more rows (padding)."""
+        learner's tensors.  `out` may hold more rows (padding).  slim=True:
+        the 128-B records without Action / HiddenState / PrevHiddenState but
+        with each row's provenance (include/mbots.h MBOTS_LEARNER_SLIM_BYTES),
+        for a learner that rebuilds those from its own writes."""
         n = self.num_agents()
-        rb = self.learner_record_bytes()
+        rb = self.learner_record_bytes(slim)
         if out is None:
             out = torch.empty((n, rb), dtype=torch.uint8, device=self.device)
         if out.dtype != torch.uint8 or out.device != self.device or not out.is_contiguous() \
                 or out.dim() != 2 or out.shape[1] != rb or out.shape[0] < n:
             raise ValueError(f"out must be a contiguous uint8 [>= {n}, {rb}] tensor on {self.device}")
-        _check(_lib.mbots_pack_learner(self._h, ctypes.c_void_p(out.data_ptr()), out.shape[0],
-                                       self._stream()))
+        fn = _lib.mbots_pack_learner_slim if slim else _lib.mbots_pack_learner
+        _check(fn(self._h, ctypes.c_void_p(out.data_ptr()), out.shape[0], self._stream()))
         return out[:n]
 
     def write_actions(self, actions=None, memory=None):

@@ -52,16 +52,19 @@ def _bitwise(a, b):
     return a.shape == b.shape and torch.equal(a.contiguous().view(torch.int32), b.contiguous().view(torch.int32))
 
 
-def _roundtrip_in_process(shards, full, steps, full_records=False):
+def _roundtrip_in_process(shards, full, steps, full_records=False, slim=False):
     """Shards and the full manager in one process: the gather / scatter data
     movement of harness/gather.py without the collectives (the reassembly and
     its inverse are the same functions).  full_records: the gathered tensors
     are also compared with the full manager's own learner records
-    (pack_learner -> unpack_learner)."""
+    (pack_learner -> unpack_learner).  slim: from the second step on the shards
+    ship slim records and Action / HiddenState / PrevHiddenState are rebuilt
+    from the learner's own writes (gather.LearnerState)."""
     sys.path.insert(0, HARNESS)
     import gather
     import madrona_bots as mb
     bad = []
+    state = gather.LearnerState() if slim else None
     for m in shards + [full]:
         m.write_synthetic_actions(1234, 0, True)
     for t in range(steps):
@@ -70,8 +73,16 @@ def _roundtrip_in_process(shards, full, steps, full_records=False):
         counts = [m.species_count_tensor().to_torch() for m in shards]
         plan = {"counts": torch.stack([c.sum(dim=0).to(torch.int64).cpu() for c in counts]),
                 "first": torch.stack([c[0].to(torch.int64).cpu() for c in counts])}
-        recs = gather.reassemble([m.pack_learner() for m in shards], plan["counts"])
-        got = mb.unpack_learner(recs)
+        use_slim = state is not None and state.ready
+        recs = gather.reassemble([m.pack_learner(slim=use_slim) for m in shards], plan["counts"])
+        if use_slim:
+            assert recs.shape[1] == shards[0].learner_record_bytes(slim=True) in (128, 192)
+            got = gather.rebuild(mb.unpack_learner(recs), gather.row_ranks(plan["counts"]), state)
+            del got["src"]
+        else:
+            got = mb.unpack_learner(recs)
+        if state is not None:
+            state.note_gathered(got)
         ref = _own_views(full)
         bad += [f"step {t}: {k}" for k in ref if not _bitwise(got[k], ref[k])]
         if full_records:
@@ -89,19 +100,52 @@ def _roundtrip_in_process(shards, full, steps, full_records=False):
             part = gather.split_rows(both, plan, r)
             assert part.shape[0] == m.num_rows()
             m.write_actions(part[:, :6].contiguous(), part[:, 6:].contiguous().view(torch.float32))
+        if state is not None:
+            state.commit(plan, actions, memory)
+    if slim:
+        assert state.ready
     return bad
 
 
+@pytest.mark.parametrize("slim", [False, True])
 @pytest.mark.parametrize("fix_depth", [False, True])
-def test_learner_roundtrip_cpu_shards_equal_one(fix_depth):
+def test_learner_roundtrip_cpu_shards_equal_one(fix_depth, slim):
     """CPU mode: 2 shards x 6 worlds (faithful rewards through the ghost) ==
-    one 12-world manager under learner-chosen actions and memory."""
+    one 12-world manager under learner-chosen actions and memory (slim: from
+    provenance records from the second step on)."""
     import madrona_bots as mb
     W = 6
     kw = dict(exec_mode="cpu", fix_depth_alias=fix_depth)
     shards = [mb.SimManager(0, W, SEED, 32, world_offset=r * W, shard_ghost=r == 0, **kw) for r in range(2)]
     full = mb.SimManager(0, 2 * W, SEED, 32, **kw)
-    assert _roundtrip_in_process(shards, full, 6) == []
+    assert _roundtrip_in_process(shards, full, 6, slim=slim) == []
+
+
+def test_provenance_rows_map_old_rows_into_the_last_global_table():
+    """gather.provenance_rows against a brute-force map: a rank's local old
+    row -> its row in the last global (species, world, slot) table."""
+    sys.path.insert(0, HARNESS)
+    import gather
+    g = torch.Generator().manual_seed(3)
+    for R in (1, 2, 5):
+        last = torch.randint(0, 6, (R, 4), generator=g)
+        last[0, 1] = 0   # an empty species segment
+        glob = {}
+        for s in range(4):
+            for r in range(R):
+                a = int(last[r, :s].sum())
+                for k in range(int(last[r, s])):
+                    glob[(r, a + k)] = len(glob)
+        cur = torch.randint(0, 6, (R, 4), generator=g)
+        owner = gather.row_ranks(cur)
+        src = []
+        for i in range(owner.shape[0]):
+            n = int(last[int(owner[i])].sum())
+            new = n == 0 or int(torch.randint(0, 5, (1,), generator=g)) == 0
+            src.append(-1 if new else int(torch.randint(0, n, (1,), generator=g)))
+        src = torch.tensor(src, dtype=torch.int32)
+        got = gather.provenance_rows(src, owner, last).tolist()
+        assert got == [-1 if o < 0 else glob[(int(owner[i]), o)] for i, o in enumerate(src.tolist())]
 
 
 def test_split_rows_inverts_reassemble():
@@ -123,7 +167,7 @@ def test_split_rows_inverts_reassemble():
     assert gather.split_rows(glob, plan, 2).shape[0] == int(cnt[2].sum())
 
 
-def _worker(rank, world, port, q, steps):
+def _worker(rank, world, port, q, steps, slim=False):
     sys.path[:0] = [HARNESS, os.path.join(ROOT, "madrona-bots_amd")]
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -137,9 +181,12 @@ def _worker(rank, world, port, q, steps):
             if m is not None:
                 m.write_synthetic_actions(1234, 0, True)
         bad = []
+        state = gather.LearnerState() if slim else None
         for t in range(steps):
             sim.step()
-            got, plan = gather.gather_learner(sim, dst=0)
+            got, plan = gather.gather_learner(sim, dst=0, state=state)
+            if got is not None:
+                got.pop("src", None)
             actions = memory = None
             if rank == 0:
                 full.step()
@@ -149,7 +196,7 @@ def _worker(rank, world, port, q, steps):
                 full.shift_observations()
                 full.write_actions(actions, memory)
             sim.shift_observations()
-            gather.scatter_actions(sim, actions, memory, plan, src=0)
+            gather.scatter_actions(sim, actions, memory, plan, src=0, state=state)
         if rank == 0:
             q.put(bad)
     finally:
@@ -172,17 +219,20 @@ def _spawn(target, world, *args):
     return q.get(timeout=5)
 
 
+@pytest.mark.parametrize("slim", [False, True])
 @pytest.mark.parametrize("world", [2, 3])
-def test_learner_roundtrip_gloo(world):
+def test_learner_roundtrip_gloo(world, slim):
     """gather_learner / scatter_actions over gloo with 2 and 3 CPU-mode ranks:
     rank 0's gathered tensors equal one manager of every world, step after
-    step, while the learner's actions drive both."""
-    assert _spawn(_worker, world, 5) == []
+    step, while the learner's actions drive both (slim: provenance records
+    and the learner's rebuild from the second step on)."""
+    assert _spawn(_worker, world, 5, slim) == []
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("slim", [False, True])
 @pytest.mark.parametrize("fix_depth", [False, True])
-def test_learner_roundtrip_hip_shards_equal_one(fix_depth):
+def test_learner_roundtrip_hip_shards_equal_one(fix_depth, slim):
     """HIP: 2 shards x 1024 worlds on the device (faithful rewards through the
     ghost) == one 2048-world manager under learner-chosen actions and memory,
     every gathered tensor bitwise, 8 steps."""
@@ -191,7 +241,7 @@ def test_learner_roundtrip_hip_shards_equal_one(fix_depth):
     kw = dict(fix_depth_alias=fix_depth)
     shards = [mb.SimManager(0, W, SEED, 32, world_offset=r * W, shard_ghost=r == 0, **kw) for r in range(2)]
     full = mb.SimManager(0, 2 * W, SEED, 32, **kw)
-    assert _roundtrip_in_process(shards, full, 8) == []
+    assert _roundtrip_in_process(shards, full, 8, slim=slim) == []
 
 
 def _rccl_worker(rank, world, port, q):
@@ -234,8 +284,8 @@ def test_learner_roundtrip_over_rccl_one_rank():
 
 @pytest.mark.gpu
 @pytest.mark.timeout(900)
-@pytest.mark.parametrize("fix_depth", [False, True])
-def test_config5_eight_shards_at_full_size(fix_depth):
+@pytest.mark.parametrize("fix_depth,slim", [(False, False), (True, False), (False, True), (True, True)])
+def test_config5_eight_shards_at_full_size(fix_depth, slim):
     """BASELINE config 5 at its own size: 262144 worlds as
     8 x 32768-world shards on one device (ranks 0..6 with their shard ghosts),
     against one 262144-world manager, 3 steps of the learner round trip of
@@ -250,5 +300,5 @@ def test_config5_eight_shards_at_full_size(fix_depth):
     kw = dict(fix_depth_alias=fix_depth)
     shards = [mb.SimManager(0, WS, SEED, 32, world_offset=r * WS, shard_ghost=r < R - 1, **kw) for r in range(R)]
     full = mb.SimManager(0, R * WS, SEED, 32, **kw)
-    assert _roundtrip_in_process(shards, full, 3, full_records=True) == []
+    assert _roundtrip_in_process(shards, full, 4 if slim else 3, full_records=True, slim=slim) == []
     assert sum(m.num_agents() for m in shards) == full.num_agents() > 8 * WS * 30
