@@ -257,6 +257,24 @@ int mbots_pack_learner_slim(mbots_handle *h, void *out, uint64_t out_rows, void 
  * prev_hidden must be NULL) and src [rows] int32 (may be NULL) */
 int mbots_unpack_learner_slim(const void *records, uint64_t rows, int32_t with_depth, int32_t device,
                               const mbots_learner_out *out, int32_t *src, void *stream);
+/* The learner rank's rebuild from slim records (no manager): for every row r
+ * of the gathered global table (species-major, per species rank-major: the
+ * reassembly of harness/gather.py) with provenance src[r] (the owning rank's
+ * row before the step, -1 new), its row g in the last global table, then
+ *   action[r] = last_action[g], hidden[r] = last_memory[g],
+ *   prev_hidden[r] = last_hidden[g]            (zeros for src = -1)
+ * -- the learner's own writes after the last step and that step's
+ * HiddenState, moved as the species sort moved the rows.  cur_counts /
+ * last_counts: [ranks][4] species rows per rank of the gathered / the last
+ * table (host memory, ranks <= MBOTS_MAX_LEARNER_RANKS).  device >= 0:
+ * every array is device memory of that GPU (16-B aligned), on `stream`;
+ * device == -1: host memory. */
+#define MBOTS_MAX_LEARNER_RANKS 32u
+int mbots_rebuild_learner(const int32_t *src, uint64_t rows, const int64_t *cur_counts,
+                          const int64_t *last_counts, uint32_t ranks, const int32_t *last_action,
+                          const float *last_memory, const float *last_hidden, uint64_t last_rows,
+                          int32_t *action, float *hidden, float *prev_hidden, int32_t device,
+                          void *stream);
 /* The learner's writes (training_loop.py:136-137: action_tensor[...] = one_hot,
  * memory_tensor[...] = new_memory) for every row at once: `rows` rows of
  * Action [rows, 6] int32 and/or HiddenState [rows, 16] f32 (either may be

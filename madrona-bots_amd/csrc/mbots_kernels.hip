@@ -2865,6 +2865,88 @@ hipError_t launch_pack_learner_slim(const SimState &S, const ObsTable &t, int pr
                        static_cast<uint8_t *>(out), out_rows);
     return hipGetLastError();
 }
+// one thread per gathered row: its old row in the last global table, then the
+// 152 B of Action / memory / hidden gathered (rows keep their relative order
+// through the sort, so the gathers are nearly contiguous)
+__global__ __launch_bounds__(256) void rebuild_learner_kernel(RebuildPlan p, const int32_t *src, uint32_t rows,
+                                                              uint32_t last_rows, const int32_t *last_action,
+                                                              const float *last_memory,
+                                                              const float *last_hidden, int32_t *action,
+                                                              float *hidden, float *prev_hidden)
+{
+    for (uint32_t r = blockIdx.x * blockDim.x + threadIdx.x; r < rows; r += gridDim.x * blockDim.x) {
+        int32_t g = rebuild_row(p, (int32_t)r, src[r]);
+        if (g >= (int32_t)last_rows) g = -1;   // (a provenance the last table does not hold: never read)
+        int2 a0 = make_int2(0, 0), a1 = a0, a2 = a0;
+        uint4 m[4], hd[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) m[k] = hd[k] = make_uint4(0u, 0u, 0u, 0u);
+        if (g >= 0) {
+            const int2 *la = reinterpret_cast<const int2 *>(last_action + (size_t)g * 6);
+            a0 = la[0];
+            a1 = la[1];
+            a2 = la[2];
+            const uint4 *lm = reinterpret_cast<const uint4 *>(last_memory + (size_t)g * kHidden);
+            const uint4 *lh = reinterpret_cast<const uint4 *>(last_hidden + (size_t)g * kHidden);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                m[k] = lm[k];
+                hd[k] = lh[k];
+            }
+        }
+        int2 *oa = reinterpret_cast<int2 *>(action + (size_t)r * 6);
+        oa[0] = a0;
+        oa[1] = a1;
+        oa[2] = a2;
+        uint4 *om = reinterpret_cast<uint4 *>(hidden + (size_t)r * kHidden);
+        uint4 *oh = reinterpret_cast<uint4 *>(prev_hidden + (size_t)r * kHidden);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            om[k] = m[k];
+            oh[k] = hd[k];
+        }
+    }
+}
+
+RebuildPlan rebuild_plan(const int64_t *cur, const int64_t *last, uint32_t ranks)
+{
+    RebuildPlan p{};
+    p.ranks = (int32_t)ranks;
+    int64_t base = 0;
+    for (int s = 0; s < 4; ++s) {   // per species: rank-major segments
+        for (uint32_t k = 0; k < ranks; ++k) {
+            p.cur_g[k][s] = (int32_t)base;
+            base += cur[k * 4 + s];
+        }
+        p.sp_end[s] = (int32_t)base;
+    }
+    int64_t lbase = 0;
+    for (int s = 0; s < 4; ++s)
+        for (uint32_t k = 0; k < ranks; ++k) {
+            p.last_g[k][s] = (int32_t)lbase;
+            lbase += last[k * 4 + s];
+        }
+    for (uint32_t k = 0; k < ranks; ++k) {
+        int64_t l = 0;
+        for (int s = 0; s < 4; ++s) {
+            p.last_l[k][s] = (int32_t)l;
+            l += last[k * 4 + s];
+        }
+    }
+    return p;
+}
+
+hipError_t launch_rebuild_learner(const RebuildPlan &p, const int32_t *src, uint32_t rows, uint32_t last_rows,
+                                  const int32_t *last_action, const float *last_memory, const float *last_hidden,
+                                  int32_t *action, float *hidden, float *prev_hidden, hipStream_t st)
+{
+    if (rows == 0) return hipSuccess;
+    const unsigned blocks = (unsigned)std::min<uint64_t>((rows + 255) / 256, 16384);
+    hipLaunchKernelGGL(rebuild_learner_kernel, dim3(blocks), dim3(256), 0, st, p, src, rows, last_rows, last_action,
+                       last_memory, last_hidden, action, hidden, prev_hidden);
+    return hipGetLastError();
+}
+
 hipError_t launch_unpack_learner_slim(const void *recs, uint32_t n, int fixd, const mbots_learner_out &o,
                                       int32_t *src, hipStream_t st)
 {

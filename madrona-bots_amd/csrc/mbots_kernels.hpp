@@ -157,5 +157,32 @@ hipError_t launch_pack_learner_slim(const SimState &S, const ObsTable &t, int pr
                                     hipStream_t st);
 hipError_t launch_unpack_learner_slim(const void *recs, uint32_t n, int fixd, const mbots_learner_out &o,
                                       int32_t *src, hipStream_t st);
+// the learner rank's rebuild of Action / HiddenState / PrevHiddenState from
+// slim records' provenance (mbots_rebuild_learner): per (rank, species) the
+// first global row of the gathered table, and of the last table with the
+// owning rank's local first row
+struct RebuildPlan {
+    int32_t ranks;
+    int32_t sp_end[4];                                  // gathered table: species segment ends
+    int32_t cur_g[MBOTS_MAX_LEARNER_RANKS][4];          // gathered: first global row of (rank, species)
+    int32_t last_l[MBOTS_MAX_LEARNER_RANKS][4];         // last table: first local row of (rank, species)
+    int32_t last_g[MBOTS_MAX_LEARNER_RANKS][4];         // last table: its first global row
+};
+RebuildPlan rebuild_plan(const int64_t *cur_counts, const int64_t *last_counts, uint32_t ranks);
+// global row of the last table for gathered row r with provenance o (-1: none)
+__host__ __device__ inline int32_t rebuild_row(const RebuildPlan &p, int32_t r, int32_t o)
+{
+    if (o < 0) return -1;
+    int s = 0;
+    while (s < 3 && r >= p.sp_end[s]) ++s;
+    int k = 0;
+    while (k + 1 < p.ranks && r >= p.cur_g[k + 1][s]) ++k;
+    int t = 3;
+    while (t > 0 && o < p.last_l[k][t]) --t;
+    return p.last_g[k][t] + (o - p.last_l[k][t]);
+}
+hipError_t launch_rebuild_learner(const RebuildPlan &p, const int32_t *src, uint32_t rows, uint32_t last_rows,
+                                  const int32_t *last_action, const float *last_memory, const float *last_hidden,
+                                  int32_t *action, float *hidden, float *prev_hidden, hipStream_t st);
 
 }  // namespace mbots

@@ -1497,6 +1497,52 @@ int mbots_unpack_learner_slim(const void *records, uint64_t rows, int32_t with_d
     return MBOTS_OK;
 }
 
+int mbots_rebuild_learner(const int32_t *src, uint64_t rows, const int64_t *cur_counts, const int64_t *last_counts,
+                          uint32_t ranks, const int32_t *last_action, const float *last_memory,
+                          const float *last_hidden, uint64_t last_rows, int32_t *action, float *hidden,
+                          float *prev_hidden, int32_t device, void *stream)
+{
+    if (!cur_counts || !last_counts || (rows && (!src || !action || !hidden || !prev_hidden)) ||
+        (last_rows && (!last_action || !last_memory || !last_hidden)))
+        return fail(MBOTS_E_INVALID, "null argument");
+    if (ranks == 0 || ranks > MBOTS_MAX_LEARNER_RANKS)
+        return fail(MBOTS_E_INVALID, "ranks must be in [1, " + std::to_string(MBOTS_MAX_LEARNER_RANKS) + "]");
+    uint64_t cur = 0, last = 0;
+    for (uint32_t i = 0; i < 4 * ranks; ++i) {
+        if (cur_counts[i] < 0 || last_counts[i] < 0) return fail(MBOTS_E_INVALID, "negative row count");
+        cur += (uint64_t)cur_counts[i];
+        last += (uint64_t)last_counts[i];
+    }
+    if (cur != rows) return fail(MBOTS_E_INVALID, "cur_counts do not sum to rows");
+    if (last != last_rows) return fail(MBOTS_E_INVALID, "last_counts do not sum to last_rows");
+    if (rows > 0x7FFFFFFFull || last_rows > 0x7FFFFFFFull) return fail(MBOTS_E_INVALID, "rows too large");
+    const mbots::RebuildPlan p = mbots::rebuild_plan(cur_counts, last_counts, ranks);
+    if (device < 0) {
+        // (a provenance outside the owning rank's last rows is refused, not read)
+        for (uint64_t r = 0; r < rows; ++r) {
+            const int32_t g = mbots::rebuild_row(p, (int32_t)r, src[r]);
+            if (g >= (int64_t)last_rows) return fail(MBOTS_E_RANGE, "provenance outside the last table");
+            for (int k = 0; k < 6; ++k) action[r * 6 + k] = g >= 0 ? last_action[(size_t)g * 6 + k] : 0;
+            for (int k = 0; k < mbots::kHidden; ++k) {
+                hidden[r * mbots::kHidden + k] = g >= 0 ? last_memory[(size_t)g * mbots::kHidden + k] : 0.0f;
+                prev_hidden[r * mbots::kHidden + k] = g >= 0 ? last_hidden[(size_t)g * mbots::kHidden + k] : 0.0f;
+            }
+        }
+        return MBOTS_OK;
+    }
+    for (const void *q : {(const void *)src, (const void *)last_action, (const void *)last_memory,
+                          (const void *)last_hidden, (const void *)action, (const void *)hidden,
+                          (const void *)prev_hidden})
+        if (reinterpret_cast<uintptr_t>(q) & 7u) return fail(MBOTS_E_INVALID, "arrays must be 8-byte aligned");
+    for (const void *q : {(const void *)last_memory, (const void *)last_hidden, (const void *)hidden,
+                          (const void *)prev_hidden})
+        if (reinterpret_cast<uintptr_t>(q) & 15u) return fail(MBOTS_E_INVALID, "float arrays must be 16-byte aligned");
+    HIP_TRY(hipSetDevice(device));
+    HIP_TRY(mbots::launch_rebuild_learner(p, src, (uint32_t)rows, (uint32_t)last_rows, last_action, last_memory,
+                                          last_hidden, action, hidden, prev_hidden, as_stream(stream)));
+    return MBOTS_OK;
+}
+
 int mbots_unpack_learner(const void *records, uint64_t rows, int32_t with_depth, int32_t device,
                          const mbots_learner_out *out, void *stream)
 {

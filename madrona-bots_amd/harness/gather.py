@@ -135,7 +135,7 @@ def gather_learner(mgr, dst=0, group=None, keys=None, state=None):
         return None, plan
     recs = reassemble([b[:n_max] for b in bufs], all_cnt)
     if slim:
-        got = rebuild(mb.unpack_learner(recs.to(dev)), row_ranks(all_cnt), state)
+        got = rebuild(mb.unpack_learner(recs.to(dev)), all_cnt, state)
     else:   # (the state keeps this step's HiddenState: every key then)
         kw = {} if keys is None or state is not None else {"keys": keys}
         got = mb.unpack_learner(recs.to(dev), **kw)
@@ -217,21 +217,13 @@ def provenance_rows(src, owner, last_counts):
     return torch.where(valid, g, torch.full_like(g, -1))
 
 
-def rebuild(got, owner, state):
+def rebuild(got, cur_counts, state):
     """Slim records: Action / HiddenState / PrevHiddenState of every gathered
     row from the learner's own last writes (LearnerState), bit-identical to
-    the manager's columns."""
-    g = provenance_rows(got["src"], owner, state.counts)
-    valid = (g >= 0)[:, None]
-    gi = g.clamp(min=0)
-
-    def take(t):
-        if t.shape[0] == 0:
-            return torch.zeros((g.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=g.device)
-        return torch.where(valid, t.index_select(0, gi), torch.zeros((), dtype=t.dtype, device=t.device))
-    got["action"] = take(state.action.to(torch.int32))
-    got["hidden"] = take(state.memory.to(torch.float32))
-    got["prev_hidden"] = take(state.hidden)
+    the manager's columns -- one native pass (madrona_bots.rebuild_learner:
+    the provenance_rows map and the three gathers)."""
+    import madrona_bots as mb
+    got.update(mb.rebuild_learner(got["src"], cur_counts, state.counts, state.action, state.memory, state.hidden))
     return got
 
 
@@ -244,7 +236,7 @@ def gather_learner_local(mgr, state=None):
     slim = state is not None and state.ready
     got = mb.unpack_learner(mgr.pack_learner(slim=slim))
     if slim:
-        got = rebuild(got, torch.zeros(got["src"].shape[0], dtype=torch.int64, device=got["src"].device), state)
+        got = rebuild(got, plan["counts"], state)
     if state is not None:
         state.note_gathered(got)
     return got, plan

@@ -26,7 +26,7 @@ import warnings
 import torch  # loads the HIP runtime libmbots.so links against (same soname)
 
 __all__ = ["SimManager", "ScriptBotsViewer", "Tensor", "madrona", "ExportID", "ExecMode", "unpack_rollout",
-           "unpack_learner", "CapacityWarning", "CapacityError", "MAX_CAPACITY"]
+           "unpack_learner", "rebuild_learner", "CapacityWarning", "CapacityError", "MAX_CAPACITY"]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB_PATH = os.path.join(_HERE, "libmbots.so")
@@ -85,6 +85,8 @@ def _load():
         "mbots_unpack_learner": [vp, ctypes.c_uint64, i32, i32, P(_LearnerOut), vp],
         "mbots_pack_learner_slim": [vp, vp, ctypes.c_uint64, vp],
         "mbots_unpack_learner_slim": [vp, ctypes.c_uint64, i32, i32, P(_LearnerOut), vp, vp],
+        "mbots_rebuild_learner": [vp, ctypes.c_uint64, vp, vp, u32, vp, vp, vp, ctypes.c_uint64, vp, vp, vp,
+                                  i32, vp],
         "mbots_write_actions": [vp, vp, vp, ctypes.c_uint64, vp],
         "mbots_num_rows": [vp, P(u32)],
         "mbots_agent_steps": [vp, P(ctypes.c_uint64)],
@@ -321,6 +323,36 @@ def unpack_learner(records, with_depth=None, keys=None):
     else:
         _check(_lib.mbots_unpack_learner(ctypes.c_void_p(rec.data_ptr()), n, 1 if depth else 0, devi,
                                          ctypes.byref(lo), stream))
+    return out
+
+
+def rebuild_learner(src, cur_counts, last_counts, last_action, last_memory, last_hidden):
+    """The learner rank's rebuild from slim records (mbots_rebuild_learner):
+    src int32 [N] (unpack_learner of slim records, in the reassembled global
+    order), cur_counts / last_counts int64 [ranks, 4] species rows per rank of
+    the gathered and of the last table, last_action int32 [M, 6] /
+    last_memory f32 [M, 16] (the learner's writes after the last step) and
+    last_hidden f32 [M, 16] (that step's HiddenState), all on one device (or
+    the host) -> {"action" [N, 6], "hidden" [N, 16], "prev_hidden" [N, 16]}:
+    the manager's Action, HiddenState and PrevHiddenState, bit-identical."""
+    dev = src.device
+    n = src.shape[0]
+    cc = torch.as_tensor(cur_counts, dtype=torch.int64).cpu().contiguous()
+    lc = torch.as_tensor(last_counts, dtype=torch.int64).cpu().contiguous()
+    if cc.dim() != 2 or cc.shape[1] != 4 or lc.shape != cc.shape:
+        raise ValueError("cur_counts / last_counts must be int64 [ranks, 4] of the same ranks")
+    la = last_action.to(device=dev, dtype=torch.int32).contiguous()
+    lm = last_memory.to(device=dev, dtype=torch.float32).contiguous()
+    lh = last_hidden.to(device=dev, dtype=torch.float32).contiguous()
+    s = src.to(torch.int32).contiguous()
+    out = {"action": torch.empty((n, 6), dtype=torch.int32, device=dev),
+           "hidden": torch.empty((n, 16), dtype=torch.float32, device=dev),
+           "prev_hidden": torch.empty((n, 16), dtype=torch.float32, device=dev)}
+    stream = ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream if dev.type == "cuda" else None)
+    ptr = lambda t: ctypes.c_void_p(t.data_ptr())   # noqa: E731
+    _check(_lib.mbots_rebuild_learner(ptr(s), n, ptr(cc), ptr(lc), cc.shape[0], ptr(la), ptr(lm), ptr(lh),
+                                      la.shape[0], ptr(out["action"]), ptr(out["hidden"]), ptr(out["prev_hidden"]),
+                                      dev.index if dev.type == "cuda" else -1, stream))
     return out
 
 

@@ -77,7 +77,7 @@ def _roundtrip_in_process(shards, full, steps, full_records=False, slim=False):
         recs = gather.reassemble([m.pack_learner(slim=use_slim) for m in shards], plan["counts"])
         if use_slim:
             assert recs.shape[1] == shards[0].learner_record_bytes(slim=True) in (128, 192)
-            got = gather.rebuild(mb.unpack_learner(recs), gather.row_ranks(plan["counts"]), state)
+            got = gather.rebuild(mb.unpack_learner(recs), plan["counts"], state)
             del got["src"]
         else:
             got = mb.unpack_learner(recs)
@@ -146,6 +146,15 @@ def test_provenance_rows_map_old_rows_into_the_last_global_table():
         src = torch.tensor(src, dtype=torch.int32)
         got = gather.provenance_rows(src, owner, last).tolist()
         assert got == [-1 if o < 0 else glob[(int(owner[i]), o)] for i, o in enumerate(src.tolist())]
+        # the native rebuild (host path of mbots_rebuild_learner) takes the same rows
+        import madrona_bots as mb
+        m = int(last.sum())
+        la = torch.randint(0, 9, (m, 6), generator=g, dtype=torch.int32)
+        lm, lh = torch.randn((m, 16), generator=g), torch.randn((m, 16), generator=g)
+        out = mb.rebuild_learner(src, cur, last, la, lm, lh)
+        for key, t in (("action", la), ("hidden", lm), ("prev_hidden", lh)):
+            want = torch.stack([t[x] if x >= 0 else torch.zeros_like(t[0]) for x in got]) if got else t[:0]
+            assert torch.equal(out[key], want), key
 
 
 def test_split_rows_inverts_reassemble():
