@@ -66,8 +66,11 @@ def algorithmic_bytes(n_agents, n_worlds):
 # B_step counts 88 B per agent the lazy shift never moves when nothing reads
 # the table between step() and shift_observations() (the 44 B of previous-obs
 # reads and the 44 B of Prev{Species,Position,Health,Surrounding,Reward,Stats}
-# writes, DESIGN.md "Lazy shift"): the bytes the bench loop must move
-LAZY_BYTES_PER_AGENT = 552.0 - 88.0
+# writes, DESIGN.md "Lazy shift"), and the 64 B of the prev-sensor move (32
+# read + 32 written), which a step owes until a reader needs it and which
+# dies at the next step (DESIGN.md "Lazy prev sensor", round 6): the bytes
+# the bench loop must move
+LAZY_BYTES_PER_AGENT = 552.0 - 88.0 - 64.0
 # the reference loop on top of B_step: construct_obs of the current and the
 # previous rows (84 B read + 276 B written each), the reward / health clones
 # (4 + 4 B each way), the learner's one-hot action + memory write (24 + 64 B)
@@ -711,7 +714,8 @@ def main():
         roof["lazy_bytes"] = {"bytes_per_agent": LAZY_BYTES_PER_AGENT, "bytes_per_step": nb_lazy,
                               "achieved": lazy_gbs, "frac": lazy_gbs / HBM_PEAK_GBS,
                               "note": "B_step minus the 88 B/agent of Prev* traffic the lazy shift "
-                                      "skips when nothing reads the table between step and shift"}
+                                      "skips when nothing reads the table between step and shift and "
+                                      "the 64 B/agent prev-sensor move nothing reads before the next step"}
         wall_gbs = nb / (elapsed / args.steps) / 1e9
         roof["wall_clock"] = {"achieved": wall_gbs, "frac": wall_gbs / HBM_PEAK_GBS,
                               "frac_lazy_bytes": nb_lazy / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBS,
