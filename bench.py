@@ -478,9 +478,6 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true",
                     help="skip the untimed per-kernel event pass after the timed region")
-    ap.add_argument("--span-every", type=int, default=8,
-                    help="bracket every k-th timed step()+shift() with HIP events (roofline "
-                         "launch duration); each event pair adds ~10 us of GPU idle")
     ap.add_argument("--full-records", action="store_true",
                     help="config 5: ship the full 272-B learner records every step (no provenance rebuild)")
     ap.add_argument("--gather", action="store_true",
@@ -550,36 +547,31 @@ def main():
         one_step(t)
     torch.cuda.synchronize()
     steps_before = mgr.agent_steps()
-    # device span of step()+shift_observations() on the launch stream (torch's
-    # current stream is the stream libmbots launches on; step() joins its
-    # internal aux stream back into it), sampled every --span-every steps
-    every = max(1, args.span_every)
-    ev = {k: (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True),
-              torch.cuda.Event(enable_timing=True))
-          for k in range(0, args.steps, every)}
+    # device time of the timed steps: an event on the launch stream (torch's
+    # current stream, the one libmbots launches on) before the first step, and
+    # the later of an event there after the last action write and one the
+    # library records after the last sensor on its own stream -- both chains
+    # of every step, no event inside the region (round 6: per-step sampled
+    # spans started at the previous action write, and so also counted the
+    # next K1's wait for the previous sensor whenever the sensor's chain was
+    # the longer one)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
 
     if distributed:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for k, t in enumerate(range(args.warmup, args.warmup + args.steps)):
-        if k in ev:
-            ev[k][0].record()
-        mgr.step()
-        mgr.shift_observations()
-        if k in ev:
-            # the span ends when both chains have: an event after shift() on
-            # this stream and one the library records after the sensor on its
-            # own stream (no join: the sampled steps run as the others do)
-            ev[k][1].record()
-            mgr.record_sensor_done(ev[k][2])
-        mgr.write_synthetic_actions(ACTION_SEED, t + 1)
+    ev[0].record()
+    for t in range(args.warmup, args.warmup + args.steps):
+        one_step(t)
+    ev[1].record()
+    mgr.record_sensor_done(ev[2])
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     if distributed:
         dist.barrier()
     elapsed = t1 - t0
-    span_ms = sum(max(a.elapsed_time(b), a.elapsed_time(c)) for a, b, c in ev.values()) / len(ev)
+    span_ms = max(ev[0].elapsed_time(ev[1]), ev[0].elapsed_time(ev[2])) / args.steps
     agent_steps = mgr.agent_steps() - steps_before
 
     # per-kernel event spans: a separate pass after the timed region (the
@@ -699,15 +691,15 @@ def main():
         }
         nb = algorithmic_bytes(mean_agents, W)
         achieved = nb / (span_ms * 1e-3) / 1e9
-        roof = {"bound": "hbm", "kernel": "world step: step()+shift_observations() "
-                "(K1 world_step, K2 scan, K3a export_rows, K4 move, K5 shift (fused gather) || K3b sensor)",
+        roof = {"bound": "hbm", "kernel": "world step: step()+shift_observations()+action write "
+                "(K1 world_step, K2 scan, K3a export_rows, K5 shift (fused gather), actions || K3b sensor)",
                 "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": achieved / HBM_PEAK_GBS, "traffic": None,
                 "algorithmic_bytes_per_launch": nb, "avg_launch_ms": span_ms,
-                "timing": f"HIP events on the launch stream around every {max(1, args.span_every)}"
-                          "th step()+shift() of the timed region, to the later of an event after "
-                          "shift() there and one recorded after the sensor on the library's stream "
-                          "(both chains of the step, no join)"}
+                "timing": "HIP events over the whole timed region / steps: one on the launch stream before "
+                          "the first step, the later of one there after the last action write and one the "
+                          "library records after the last sensor on its own stream (both chains, no event "
+                          "inside the region)"}
         # the same span priced at the bytes this design must move in this loop
         nb_lazy = LAZY_BYTES_PER_AGENT * mean_agents + 1952.0 * W
         lazy_gbs = nb_lazy / (span_ms * 1e-3) / 1e9

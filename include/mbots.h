@@ -361,12 +361,12 @@ const char *mbots_last_error(void);
  *   MBOTS_SERIALISING_ENV is set (non-empty, not "0") when the manager is
  *   created: rocprofv3 counter collection, an HSA tools library, a legacy
  *   rocprof input file, or serialised kernel dispatch.
- * MBOTS_SWAP=1 (read at mbots_create; above 8192 worlds): K1 and K2 run on
- *   the internal stream before the sensor, with no cross-stream hop between
- *   them, and the caller's stream joins after K2 for the export rows.  Faster
- *   once the sensor's chain sets the pace (-2.4 % at 65536 worlds with every
- *   world's food at its cap), slower early in a run (+0.6 to +1.2 % over steps
- *   5-24), so it is off by default.
+ * MBOTS_SWAP (read at mbots_create; above 8192 worlds): by default ("1") K1
+ *   and K2 run on the internal stream before the sensor, with no cross-stream
+ *   hop between them, and the caller's stream joins after K2 for the export
+ *   rows (the sensor's chain sets the step's pace: -2 % against the forked
+ *   schedule); MBOTS_SWAP=0 keeps K1 and K2 on the caller's stream and forks
+ *   the sensor off after K2.
  * MBOTS_CPU_THREADS: host threads of MBOTS_EXEC_CPU (default: the machine's
  *   hardware threads, at most 16).
  * MBOTS_EPOCH_START=<n> (read at mbots_create; a test hook): the value waits

@@ -126,8 +126,9 @@ struct mbots_handle {
     bool prev_lazy[2] = {false, false};   // table half's six shift-owned Prev* columns are
                                           // still its current ones (lazy shift, K5)
     hipEvent_t ev_hop = nullptr;      // orders a call's stream after the last one used
-    // MBOTS_SWAP=1 (large world counts): K1 and K2 on the sensor's stream, the
-    // caller's stream joining after K2 (DESIGN.md 4 "Which chain sets the pace")
+    // the swapped schedule (above 8192 worlds unless MBOTS_SWAP=0): K1 and K2 on
+    // the sensor's stream, the caller's stream joining after K2 (DESIGN.md 4
+    // "Which chain sets the pace")
     bool swap = false;
     hipEvent_t ev_caller = nullptr;   // the caller's stream at a step's start
     uint32_t *sig_fork = nullptr;     // the fork's signal word (small world counts)
@@ -167,6 +168,9 @@ namespace {
 #endif
 #ifndef MB_VALUE_JOIN_MAX
 #define MB_VALUE_JOIN_MAX 8192
+#endif
+#ifndef MB_SWAP_DEFAULT
+#define MB_SWAP_DEFAULT 1   // MBOTS_SWAP's default (large world counts)
 #endif
 #ifndef MB_VALUE_ADAPT
 #define MB_VALUE_ADAPT 1   // value waits only while the host runs ahead of the device
@@ -850,8 +854,16 @@ int mbots_create(const mbots_config *cfg_in, mbots_handle **out)
         if (const char *e = std::getenv("MBOTS_EPOCH_START"))
             h->epoch = std::min<uint32_t>((uint32_t)std::strtoul(e, nullptr, 0), kEpochWrap);
     }
-    if (const char *e = std::getenv("MBOTS_SWAP"))
-        h->swap = e[0] == '1' && S.W > MB_VALUE_FORK_MAX && !h->k1_finder && !h->sig_fork && !h->sig_join;
+    {
+        // (the default above 8192 worlds since round 6: with the prev-sensor
+        // move lazy the caller's chain is the shorter one from the first steps
+        // on, and the swap takes both hops off the sensor's chain: -1.9 % in
+        // the driver's window, -2.1 % at steady state, interleaved on one box;
+        // MBOTS_SWAP=0 restores the forked schedule)
+        const char *e = std::getenv("MBOTS_SWAP");
+        const bool want = e && *e ? e[0] == '1' : MB_SWAP_DEFAULT != 0;
+        h->swap = want && S.W > MB_VALUE_FORK_MAX && !h->k1_finder && !h->sig_fork && !h->sig_join;
+    }
     if (h->swap) check(hipEventCreateWithFlags(&h->ev_caller, kSyncEvent), "hipEventCreateWithFlags");
     check(hipEventCreateWithFlags(&h->ev_join[0], kSyncEvent), "hipEventCreateWithFlags");
     check(hipEventCreateWithFlags(&h->ev_join[1], kSyncEvent), "hipEventCreateWithFlags");

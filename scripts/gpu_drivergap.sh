@@ -26,6 +26,6 @@ timeout -k 10 120 python3 -u scripts/steptrace.py --steps 300 > $O/trace.json 2>
 run s20w5 --steps 20 --warmup 5 --no-secondary --no-cpu-baseline
 run s100w20 --steps 100 --warmup 20 --no-secondary --no-cpu-baseline
 run s20w100 --steps 20 --warmup 100 --no-secondary --no-cpu-baseline
-run s20w5_nospan --steps 20 --warmup 5 --span-every 1000 --no-secondary --no-cpu-baseline
+run s20w5_nospan --steps 20 --warmup 5 --no-secondary --no-cpu-baseline
 run s100w5 --steps 100 --warmup 5 --no-secondary --no-cpu-baseline
 run driver2 --gpus 1 --steps 20 --warmup 5

@@ -114,15 +114,19 @@ def test_learner_pattern_long_horizon_4096():
     _run(4096, 20, True, True, seed=77)
 
 
-def test_learner_pattern_swap_schedule_16384(monkeypatch):
-    """MBOTS_SWAP=1 (K1 / K2 / the sensor on the internal stream) under the
-    training loop's pattern, then a checkpoint hand-over in the middle of the
-    loop into a fresh MBOTS_SWAP=1 manager, then more of the pattern: every
-    read and every column equal the oracle's."""
+@pytest.mark.parametrize("swap", ["1", "0"])
+def test_learner_pattern_swap_schedule_16384(monkeypatch, swap):
+    """Both large-world schedules -- K1 / K2 / the sensor on the internal
+    stream (MBOTS_SWAP=1, the default above 8192 worlds) and the sensor forked
+    off the caller's stream (MBOTS_SWAP=0) -- under the training loop's
+    pattern, then a checkpoint hand-over in the middle of the loop into a
+    fresh manager of the same schedule, then more of the pattern: every read
+    and every column equal the oracle's."""
     import madrona_bots as mb
     W = 16384
-    monkeypatch.setenv("MBOTS_SWAP", "1")   # read when a manager is created
+    monkeypatch.setenv("MBOTS_SWAP", swap)   # read when a manager is created
     mgr = mb.SimManager(0, W, 69, 32)
+    assert mgr.schedule_info()["swap"] == (swap == "1")
     ref = OracleSimManager(0, W, 69, 32, num_threads=16)
     gg = torch.Generator().manual_seed(5)
     go = torch.Generator().manual_seed(5)
@@ -145,14 +149,16 @@ def test_learner_pattern_swap_schedule_16384(monkeypatch):
     assert not errs, errs[:5]
 
 
-def test_swap_schedule_graph_capture_16384(monkeypatch):
+@pytest.mark.parametrize("swap", ["1", "0"])
+def test_swap_schedule_graph_capture_16384(monkeypatch, swap):
     """A graph-captured pair of steps (with the synthetic writer) replayed on
-    a manager created under MBOTS_SWAP=1, after eager swap-schedule steps: the
-    replays equal the same sequence on the oracle, bitwise."""
+    a manager of either large-world schedule, after eager steps: the replays
+    equal the same sequence on the oracle, bitwise."""
     import madrona_bots as mb
     W = 16384
-    monkeypatch.setenv("MBOTS_SWAP", "1")
+    monkeypatch.setenv("MBOTS_SWAP", swap)
     mgr = mb.SimManager(0, W, 69, 32)
+    assert mgr.schedule_info()["swap"] == (swap == "1")
     monkeypatch.delenv("MBOTS_SWAP", raising=False)
     orc = pyoracle.OracleSim(W, 69, 32, num_threads=16)
     s = torch.cuda.Stream()
