@@ -169,6 +169,9 @@ namespace {
 #ifndef MB_VALUE_JOIN_MAX
 #define MB_VALUE_JOIN_MAX 8192
 #endif
+#ifndef MB_FINDER_PSEM_BY_SENSOR
+#define MB_FINDER_PSEM_BY_SENSOR 1   // K1-finder mode: the sensor moves the prev-sensor rows itself
+#endif
 #ifndef MB_SWAP_DEFAULT
 #define MB_SWAP_DEFAULT 1   // MBOTS_SWAP's default (large world counts)
 #endif
@@ -1085,7 +1088,7 @@ int mbots_step(mbots_handle *h, void *stream)
     else HIP_TRY(hipStreamWaitEvent(h->aux, h->ev_totals, 0));
     // (K1-finder mode: the sensor also moves the last table's sensor rows into
     // its rows' prev-sensor columns, so no caller-stream wait is needed for them)
-    const bool psem_by_sensor = h->k1_finder;
+    const bool psem_by_sensor = h->k1_finder && MB_FINDER_PSEM_BY_SENSOR;
     if (psem_by_sensor) {
         h->S.psem_src = h->T[h->tb].sem;
         h->S.pdepth_src = (h->cfg.flags & MBOTS_FLAG_FIX_DEPTH_ALIAS) ? h->T[h->tb].depth : nullptr;
@@ -1110,8 +1113,11 @@ int mbots_step(mbots_handle *h, void *stream)
     if ((rc = timed(h, MBOTS_TK_EXPORT, st,
                     [&] { return mbots::launch_export_rows(h->S, nxt, 0, st); })))
         return rc;
-    // (the prev sensor is the sensor's own part in K1-finder mode)
+    // (the prev sensor is the sensor's own part in K1-finder mode; moved here
+    // instead, its source rows are the last sensor's, which this step's K1 did
+    // not wait for in that mode)
     if (psem_by_sensor) prefetch &= ~mbots::kMoveSensor;
+    if ((prefetch & mbots::kMoveSensor) && (rc = wait_prev_sensor(h, st))) return rc;
     if (prefetch && (rc = timed(h, MBOTS_TK_MOVE, st, [&] {
                          return mbots::launch_move(h->S, cur, nxt, lazy, prefetch, st);
                      })))

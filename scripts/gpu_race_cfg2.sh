@@ -1,0 +1,19 @@
+#!/bin/bash
+# GPU box: the K1-finder prev-sensor race test against a single-buffered
+# obsrow_out build (expected to fail) and the tree's library, then the
+# small-world schedule sizing.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+PYTHONPATH=scripts MBOTS_LIB=build_var/libmbots_single.so timeout -k 10 300 python -u -m pytest -p _variant \
+    tests/test_parity_gpu.py -k "k1_finder_step_only" -v --timeout 200 --timeout-method thread -p no:warnings \
+    > gpurun_out/race_single.log 2>&1
+echo "single-buffer build rc=$? (1: the test caught the race)"
+grep -E "PASSED|FAILED" gpurun_out/race_single.log | head
+timeout -k 10 300 python -u -m pytest tests/test_parity_gpu.py -k "k1_finder_step_only" -v --timeout 200 \
+    --timeout-method thread -p no:warnings > gpurun_out/race_tree.log 2>&1 || { tail -20 gpurun_out/race_tree.log; exit 1; }
+grep -E "PASSED|FAILED" gpurun_out/race_tree.log | head
+LIBS="build_var/libmbots_f8192.so build_var/libmbots_f8192lazy.so build_var/libmbots_flazy.so" \
+    bash scripts/gpu_cfg2_ab.sh > gpurun_out/cfg2_ab.log 2>&1 || exit 1
+python scripts/ab_parse.py gpurun_out/cfg2_ab.log

@@ -63,24 +63,27 @@ def test_parity_population_order(cap, depth_fixed):
     _pair(2048, steps=4, cap=cap, depth_fixed=depth_fixed)
 
 
-@pytest.mark.parametrize("cap,depth_fixed,shift", [(256, True, False), (256, False, True), (128, True, True)])
-def test_k1_finder_step_only_prev_sensor(cap, depth_fixed, shift):
+@pytest.mark.parametrize("cap,A,depth_fixed,shift", [(256, 96, True, False), (256, 96, False, True),
+                                                     (128, 32, True, True)])
+def test_k1_finder_step_only_prev_sensor(cap, A, depth_fixed, shift):
     """in K1-finder mode (<= 2048 worlds) the next K1 waits
     only for the sensor before the last one, while the sensor reads K1's
     old-row column (obsrow_out) to move the previous sensor rows into its own
     rows -- so that column is double-buffered by step parity.  Steps back to
     back with no read in between (the bench's loop: actions, step, optionally
     the shift) at 2048 worlds, where the sensor's waves take more than one
-    residency round (256 slots and the depth bytes lower its occupancy); after
-    each burst every column, the prev sensor's semantic and depth included,
-    equals the oracle's."""
+    residency round (256 slots and the depth bytes lower its occupancy) and,
+    with 96 agents per world, takes several times the next K1's time, so that
+    K1 runs while the sensor's last blocks are still to start; after each
+    burst every column, the prev sensor's semantic and depth included, equals
+    the oracle's."""
     import madrona_bots as mb
     W = 2048
-    mgr = mb.SimManager(0, W, 69, 32, agent_capacity=cap, fix_depth_alias=depth_fixed)
-    orc = pyoracle.OracleSim(W, 69, 32, cap=cap, num_threads=8)
+    mgr = mb.SimManager(0, W, 69, A, agent_capacity=cap, fix_depth_alias=depth_fixed)
+    orc = pyoracle.OracleSim(W, 69, A, cap=cap, num_threads=16)
     t = 0
-    for burst in range(3):
-        for _ in range(6):
+    for burst in range(2):
+        for _ in range(5):
             mgr.write_synthetic_actions(1234, t, True)
             orc.write_synthetic_actions(1234, t, True)
             mgr.step()
