@@ -246,8 +246,8 @@ int mbots_unpack_learner(const void *records, uint64_t rows, int32_t with_depth,
  *         128..191  depth, prev depth (uint8 x 32 each), only with
  *                   MBOTS_FLAG_FIX_DEPTH_ALIAS
  * The rebuilt columns equal the manager's as long as every row's Action and
- * HiddenState were written after the last step and one or more shifts
- * separate the two steps (the learner's loop).  mbots_pack_learner_slim
+ * HiddenState were written after the last step, after its shift(s) (the
+ * learner's loop: step, gather, shift, write).  mbots_pack_learner_slim
  * moves none of the step's deferred columns: the previous observation rows
  * the step still owes are gathered inside its launch. */
 #define MBOTS_LEARNER_SLIM_BYTES        128u

@@ -162,7 +162,8 @@ class LearnerState:
     with A_{t-1} / M_{t-1} the actions and memory scattered after step t-1 and
     src mapped from the owning rank's old rows into the last global table
     (that step's plan).  Valid while every row's action and memory are written
-    after every step (scatter_actions does) -- after any other write, a
+    after every step, after its shift(s) (scatter_actions does; a shift
+    between per-species writes, SURVEY B.9, breaks it) -- after any other write, a
     checkpoint load or a new manager, call reset() on every rank: the next
     gather then ships full records again.  Every rank holds one (they agree on
     the record width); only the learner rank holds tensors.  The learner must
