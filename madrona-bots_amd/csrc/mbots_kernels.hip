@@ -1030,8 +1030,8 @@ __global__ __launch_bounds__(256) void export_rows_kernel(SimState S, ObsTable n
     constexpr bool init = kInit;
     const uint32_t wv = threadIdx.x >> 6;
     const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t nwv = gridDim.x * kWorldsPerBlock;
-    for (uint32_t w = uniform(blockIdx.x * kWorldsPerBlock + wv); w < S.W; w += nwv) {
+    const uint32_t w = uniform(blockIdx.x * kWorldsPerBlock + wv);
+    if (w >= S.W) return;
     const size_t base = (size_t)w * S.cap;
     const int n = uniform(S.n[w]);
     // slot `lane`'s species loaded beside the count (rows past n are stale
@@ -1098,7 +1098,6 @@ __global__ __launch_bounds__(256) void export_rows_kernel(SimState S, ObsTable n
             if (stv.y) rv += 15.0f;
         }
         st_stream(nxt.reward + r, rv, nt);
-    }
     }
 }
 
@@ -2493,17 +2492,14 @@ __global__ __launch_bounds__(256) void init_kernel(SimState S)
 // ---------------------------------------------------------------------------
 // Harness: identity-keyed synthetic action stream
 // ---------------------------------------------------------------------------
-#ifndef MB_ACT_WORLDS_PER_WAVE
-#define MB_ACT_WORLDS_PER_WAVE 1   // worlds one wave of the writer takes in turn
-#endif
 __global__ __launch_bounds__(256) void synthetic_actions_kernel(SimState S, ObsTable t,
                                                                 uint32_t seed, uint32_t step,
                                                                 int write_hidden)
 {
     const uint32_t wv = threadIdx.x >> 6;
     const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t nw = gridDim.x * kWorldsPerBlock;
-    for (uint32_t w = uniform(blockIdx.x * kWorldsPerBlock + wv); w < S.W; w += nw) {
+    const uint32_t w = uniform(blockIdx.x * kWorldsPerBlock + wv);
+    if (w >= S.W) return;
     const size_t base = (size_t)w * S.cap;
     const uint32_t gw = S.world_offset + w;
     const int n = uniform(S.n[w]);
@@ -2536,7 +2532,6 @@ __global__ __launch_bounds__(256) void synthetic_actions_kernel(SimState S, ObsT
                     make_float2(u01(d.x) - 0.5f, u01(d.y) - 0.5f);
             }
         }
-    }
     }
 }
 
@@ -2632,14 +2627,10 @@ hipError_t launch_scan(const SimState &S, int parity, hipStream_t st, hipEvent_t
     hipExtLaunchKernelGGL(scan_kernel, dim3(S.ntiles), dim3(1024), 0, st, nullptr, done, 0u, S, parity);
     return hipGetLastError();
 }
-#ifndef MB_EXPORT_WORLDS_PER_WAVE
-#define MB_EXPORT_WORLDS_PER_WAVE 1   // worlds one K3a wave takes in turn
-#endif
 hipError_t launch_export_rows(const SimState &S, const ObsTable &nxt, int init, hipStream_t st)
 {
-    const unsigned blocks = (world_blocks(S.W) + MB_EXPORT_WORLDS_PER_WAVE - 1) / MB_EXPORT_WORLDS_PER_WAVE;
     if (init) hipLaunchKernelGGL(export_rows_kernel<true>, dim3(world_blocks(S.W)), dim3(256), 0, st, S, nxt);
-    else hipLaunchKernelGGL(export_rows_kernel<false>, dim3(blocks), dim3(256), 0, st, S, nxt);
+    else hipLaunchKernelGGL(export_rows_kernel<false>, dim3(world_blocks(S.W)), dim3(256), 0, st, S, nxt);
     return hipGetLastError();
 }
 #if defined(MB_PROBE_SHIFT) && !defined(MB_PROBE_BUILD)
@@ -2760,8 +2751,8 @@ hipError_t launch_shift(const SimState &S, const ObsTable &t, int mode, hipStrea
 hipError_t launch_synthetic_actions(const SimState &S, const ObsTable &t, uint32_t seed,
                                     uint32_t step, int write_hidden, hipStream_t st)
 {
-    const unsigned blocks = (world_blocks(S.W) + MB_ACT_WORLDS_PER_WAVE - 1) / MB_ACT_WORLDS_PER_WAVE;
-    hipLaunchKernelGGL(synthetic_actions_kernel, dim3(blocks), dim3(256), 0, st, S, t, seed, step, write_hidden);
+    hipLaunchKernelGGL(synthetic_actions_kernel, dim3(world_blocks(S.W)), dim3(256), 0, st, S, t,
+                       seed, step, write_hidden);
     return hipGetLastError();
 }
 hipError_t launch_construct_obs(const SimState &S, const ObsTable &t, int prev, int prev_lazy,

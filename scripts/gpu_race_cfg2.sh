@@ -6,6 +6,8 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
+timeout -k 10 60 ./scripts/ubench/valu_rate > gpurun_out/valu_rate.jsonl 2>&1 || exit 1
+cat gpurun_out/valu_rate.jsonl
 PYTHONPATH=scripts MBOTS_LIB=build_var/libmbots_single.so timeout -k 10 300 python -u -m pytest -p _variant \
     tests/test_parity_gpu.py -k "k1_finder_step_only" -v --timeout 200 --timeout-method thread -p no:warnings \
     > gpurun_out/race_single.log 2>&1

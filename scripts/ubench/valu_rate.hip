@@ -38,6 +38,24 @@ __global__ __launch_bounds__(256) void valu_kernel(float *out, int iters, float 
             x6 = __builtin_amdgcn_sqrtf(x6); x7 = __builtin_amdgcn_sqrtf(x7);
         } else if constexpr (kMode == 7) {   // 8 independent multiplies
             x0 *= a; x1 *= b; x2 *= a; x3 *= b; x4 *= a; x5 *= b; x6 *= a; x7 *= b;
+        } else if constexpr (kMode == 8) {   // 4 independent packed f16 FMAs (2 halves each)
+            typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+            h2 p0 = {(_Float16)x0, (_Float16)x1}, p1 = {(_Float16)x2, (_Float16)x3};
+            h2 p2 = {(_Float16)x4, (_Float16)x5}, p3 = {(_Float16)x6, (_Float16)x7};
+            const h2 va = {(_Float16)a, (_Float16)a}, vb = {(_Float16)b, (_Float16)b};
+            for (int k = 0; k < 4; ++k) {
+                p0 = __builtin_elementwise_fma(p0, va, vb); p1 = __builtin_elementwise_fma(p1, va, vb);
+                p2 = __builtin_elementwise_fma(p2, va, vb); p3 = __builtin_elementwise_fma(p3, va, vb);
+            }
+            x0 = (float)p0.x; x1 = (float)p0.y; x2 = (float)p1.x; x3 = (float)p1.y;
+            x4 = (float)p2.x; x5 = (float)p2.y; x6 = (float)p3.x; x7 = (float)p3.y;
+        } else if constexpr (kMode == 9) {   // 8 independent f32 compares to lane masks, OR-combined
+            uint64_t m = 0;
+            m |= __builtin_amdgcn_fcmpf(x0, a, 5); m |= __builtin_amdgcn_fcmpf(x1, b, 5);
+            m |= __builtin_amdgcn_fcmpf(x2, a, 5); m |= __builtin_amdgcn_fcmpf(x3, b, 5);
+            m |= __builtin_amdgcn_fcmpf(x4, a, 5); m |= __builtin_amdgcn_fcmpf(x5, b, 5);
+            m |= __builtin_amdgcn_fcmpf(x6, a, 5); m |= __builtin_amdgcn_fcmpf(x7, b, 5);
+            x0 += (float)(m & 1u);
         } else {   // compare + select pairs (VOPC to vcc / SGPR + v_cndmask)
             x0 = x0 < a ? x0 + b : x0 - b; x1 = x1 < a ? x1 + b : x1 - b;
             x2 = x2 < a ? x2 + b : x2 - b; x3 = x3 < a ? x3 + b : x3 - b;
@@ -75,6 +93,8 @@ int main()
     run<5>("fma x6 + rcp x2", 8, out);
     run<6>("sqrt x8", 8, out);
     run<7>("mul x8", 8, out);   // per pair: v_cmp, v_add, v_sub, v_cndmask ~ 3 VALU
+    run<8>("pk_fma_f16 x16 (32 f16 FMAs; + 8 cvt in / 8 out per 4 iters)", 16, out);
+    run<9>("cmp-to-mask x8 (+1 add)", 9, out);
     hipFree(out);
     return 0;
 }
