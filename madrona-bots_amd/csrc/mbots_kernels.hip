@@ -1025,13 +1025,9 @@ __global__ __launch_bounds__(1024) void tile_sum_kernel(SimState S, int parity)
 // the K4 move stream.
 // ---------------------------------------------------------------------------
 template <bool kInit>
-__global__ __launch_bounds__(256) void export_rows_kernel(SimState S, ObsTable nxt)
+__device__ __forceinline__ void export_world(const SimState &S, const ObsTable &nxt, uint32_t w, uint32_t lane)
 {
     constexpr bool init = kInit;
-    const uint32_t wv = threadIdx.x >> 6;
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t w = uniform(blockIdx.x * kWorldsPerBlock + wv);
-    if (w >= S.W) return;
     const size_t base = (size_t)w * S.cap;
     const int n = uniform(S.n[w]);
     // slot `lane`'s species loaded beside the count (rows past n are stale
@@ -1098,6 +1094,22 @@ __global__ __launch_bounds__(256) void export_rows_kernel(SimState S, ObsTable n
             if (stv.y) rv += 15.0f;
         }
         st_stream(nxt.reward + r, rv, nt);
+    }
+}
+
+#ifndef MB_EXPORT_WPW
+#define MB_EXPORT_WPW 1   // worlds per K3a wave (straight-line: each its own unrolled body)
+#endif
+template <bool kInit>
+__global__ __launch_bounds__(256) void export_rows_kernel(SimState S, ObsTable nxt)
+{
+    const uint32_t wv = threadIdx.x >> 6;
+    const uint32_t lane = threadIdx.x & 63u;
+    constexpr int kWpw = kInit ? 1 : MB_EXPORT_WPW;
+#pragma unroll
+    for (int k = 0; k < kWpw; ++k) {
+        const uint32_t w = uniform((blockIdx.x * kWpw + k) * kWorldsPerBlock + wv);
+        if (w < S.W) export_world<kInit>(S, nxt, w, lane);
     }
 }
 
@@ -2492,14 +2504,9 @@ __global__ __launch_bounds__(256) void init_kernel(SimState S)
 // ---------------------------------------------------------------------------
 // Harness: identity-keyed synthetic action stream
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void synthetic_actions_kernel(SimState S, ObsTable t,
-                                                                uint32_t seed, uint32_t step,
-                                                                int write_hidden)
+__device__ __forceinline__ void synthetic_actions_world(const SimState &S, const ObsTable &t, uint32_t seed,
+                                                        uint32_t step, int write_hidden, uint32_t w, uint32_t lane)
 {
-    const uint32_t wv = threadIdx.x >> 6;
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t w = uniform(blockIdx.x * kWorldsPerBlock + wv);
-    if (w >= S.W) return;
     const size_t base = (size_t)w * S.cap;
     const uint32_t gw = S.world_offset + w;
     const int n = uniform(S.n[w]);
@@ -2532,6 +2539,22 @@ __global__ __launch_bounds__(256) void synthetic_actions_kernel(SimState S, ObsT
                     make_float2(u01(d.x) - 0.5f, u01(d.y) - 0.5f);
             }
         }
+    }
+}
+
+#ifndef MB_ACT_WPW
+#define MB_ACT_WPW 1   // worlds per writer wave (straight-line: each its own unrolled body)
+#endif
+__global__ __launch_bounds__(256) void synthetic_actions_kernel(SimState S, ObsTable t,
+                                                                uint32_t seed, uint32_t step,
+                                                                int write_hidden)
+{
+    const uint32_t wv = threadIdx.x >> 6;
+    const uint32_t lane = threadIdx.x & 63u;
+#pragma unroll
+    for (int k = 0; k < MB_ACT_WPW; ++k) {
+        const uint32_t w = uniform((blockIdx.x * MB_ACT_WPW + k) * kWorldsPerBlock + wv);
+        if (w < S.W) synthetic_actions_world(S, t, seed, step, write_hidden, w, lane);
     }
 }
 
@@ -2630,7 +2653,8 @@ hipError_t launch_scan(const SimState &S, int parity, hipStream_t st, hipEvent_t
 hipError_t launch_export_rows(const SimState &S, const ObsTable &nxt, int init, hipStream_t st)
 {
     if (init) hipLaunchKernelGGL(export_rows_kernel<true>, dim3(world_blocks(S.W)), dim3(256), 0, st, S, nxt);
-    else hipLaunchKernelGGL(export_rows_kernel<false>, dim3(world_blocks(S.W)), dim3(256), 0, st, S, nxt);
+    else hipLaunchKernelGGL(export_rows_kernel<false>, dim3((world_blocks(S.W) + MB_EXPORT_WPW - 1) / MB_EXPORT_WPW),
+                            dim3(256), 0, st, S, nxt);
     return hipGetLastError();
 }
 #if defined(MB_PROBE_SHIFT) && !defined(MB_PROBE_BUILD)
@@ -2751,8 +2775,8 @@ hipError_t launch_shift(const SimState &S, const ObsTable &t, int mode, hipStrea
 hipError_t launch_synthetic_actions(const SimState &S, const ObsTable &t, uint32_t seed,
                                     uint32_t step, int write_hidden, hipStream_t st)
 {
-    hipLaunchKernelGGL(synthetic_actions_kernel, dim3(world_blocks(S.W)), dim3(256), 0, st, S, t,
-                       seed, step, write_hidden);
+    hipLaunchKernelGGL(synthetic_actions_kernel, dim3((world_blocks(S.W) + MB_ACT_WPW - 1) / MB_ACT_WPW), dim3(256),
+                       0, st, S, t, seed, step, write_hidden);
     return hipGetLastError();
 }
 hipError_t launch_construct_obs(const SimState &S, const ObsTable &t, int prev, int prev_lazy,
