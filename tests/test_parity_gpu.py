@@ -309,7 +309,7 @@ def _obs_rows_oracle(orc, prev, fixd):
 
 
 @pytest.mark.parametrize("seed", list(range(1, 13)))
-def test_random_call_sequences(seed):
+def test_random_call_sequences(seed, W=None):
     """Random interleavings of step / shift / action writes / single-column
     reads / fused learner rows (construct_obs, current or previous) /
     checkpoint hand-overs against the oracle.  Each read materialises one
@@ -322,7 +322,8 @@ def test_random_call_sequences(seed):
     from simpair import COLUMNS, bits, gpu_column
     import madrona_bots as mb
     rng = np.random.default_rng(seed)
-    W, fixd = (4100 if seed % 4 == 0 else 20 + seed), bool(seed % 2)
+    W = W or (4100 if seed % 4 == 0 else 20 + seed)
+    fixd = bool(seed % 2)
     mgr = mb.SimManager(0, W, 69, 32, fix_depth_alias=fixd)
     orc = pyoracle.OracleSim(W, 69, 32, num_threads=8)
     t = 0
@@ -363,6 +364,14 @@ def test_random_call_sequences(seed):
             assert not errs, errs[:5]
     errs = compare(mgr, orc, "end", depth_fixed=fixd)
     assert not errs, errs[:5]
+
+
+@pytest.mark.parametrize("seed", [101, 102])
+def test_random_call_sequences_swapped_schedule(seed):
+    """The random call sequences at 16400 worlds, on the swapped schedule
+    (K1 / K2 / the sensor on the internal stream: the default above 8192
+    worlds) with the lazy prev-sensor move."""
+    test_random_call_sequences(seed, W=16400)
 
 
 @pytest.mark.parametrize("ops", ["hss" + "wss" * 9, "hsswss" + "ss" * 4 + "wsw", "sss" + "hss" * 6,
