@@ -32,7 +32,9 @@ constexpr int kWorldsPerBlock = 4;
 constexpr int kTileWorlds = 1024;             // worlds per scan tile (K2 block)
 
 #ifndef MB_SHIFT_UNROLL
-#define MB_SHIFT_UNROLL 1   // items per thread per pass of the fused shift
+#define MB_SHIFT_UNROLL 2   // items per thread per pass of the fused shift (2 vs 1: the
+                            // driver's window -1.5 %, steady state +-0; 4 and 8 with
+                            // proportionally fewer blocks +1 / +7 %: DESIGN_EXPERIMENTS r6)
 #endif
 #ifndef MB_NT
 #define MB_NT 35  // non-temporal stores: 1 K4, 2 K5, 4 K3a, 8 sensor output;
