@@ -454,8 +454,11 @@ void Sim::sensor_world(uint32_t w, Table &nxt)
     for (int i = 0; i < n; ++i) {
         const float ax = x_[base + i], ay = y_[base + i];
         const float2 h = hd[i];
-        uint32_t key[kRays];
-        for (int k = 0; k < kRays; ++k) key[k] = kNoKey;
+        // 64-bit keys in every capacity class (mbots_ray.hpp Key<>: the same
+        // (depth, order) minimum as the device's 32-bit keys up to 256 slots)
+        using K = uint64_t;
+        K key[kRays];
+        for (int k = 0; k < kRays; ++k) key[k] = Key<K>::none;
         auto fl_of = [&](float px, float py, float &f, float &l) {
             const float vx = px - ax, vy = py - ay;
             f = vx * h.x + vy * h.y;
@@ -468,10 +471,10 @@ void Sim::sensor_world(uint32_t w, Table &nxt)
             const uint32_t order = kOrderFood + (uint32_t)j;
             for (int k = 0; k < kSensor; ++k) {
                 const bool fwd = k < 24;
-                if (box_hit(b, ray_u(k), fwd, np[k].c)) key[k] = std::min(key[k], zkey(box_z(b, fwd), order));
+                if (box_hit(b, ray_u(k), fwd, np[k].c)) key[k] = std::min(key[k], Key<K>::make(box_z(b, fwd), order));
             }
             if (box_hit(b, 0.0f, true, np[kSensor].c))
-                key[kSensor] = std::min(key[kSensor], zkey(box_z(b, true), order));
+                key[kSensor] = std::min(key[kSensor], Key<K>::make(box_z(b, true), order));
         }
         for (int j = 0; j < n; ++j) {
             if (j == i) continue;
@@ -479,8 +482,8 @@ void Sim::sensor_world(uint32_t w, Table &nxt)
             fl_of(x_[base + j], y_[base + j], f, l);
             const uint32_t order = kOrderAgent + (uint32_t)j;
             for (int k = 0; k < kSensor; ++k)
-                key[k] = std::min(key[k], pixel_key(f, l, ray_u(k), np[k], k < 24, order));
-            key[kSensor] = std::min(key[kSensor], finder_key(f, l, order));
+                key[k] = std::min(key[k], pixel_key<K>(f, l, ray_u(k), np[k], k < 24, order));
+            key[kSensor] = std::min(key[kSensor], finder_key<K>(f, l, order));
         }
         // each ray's near point: in the inner rectangle (the wall is the exit
         // from it), inside a wall box (the wall, at s0) or beyond (a miss)
@@ -493,11 +496,11 @@ void Sim::sensor_world(uint32_t w, Table &nxt)
             const bool fwd = k < 24;
             const float u = ray_u(k), sgn = fwd ? 1.0f : -1.0f;
             const float dx = sgn * (h.x + u * h.y), dy = sgn * (h.y + u * (-h.x));
-            const uint32_t kv = key[k];
-            const float oz = u2f(kv & ~kOrderMask);
-            const uint32_t order = kv & kOrderMask;
+            const K kv = key[k];
+            const float oz = Key<K>::z(kv);
+            const uint32_t order = Key<K>::order(kv);
             const int cls = cls_of(k, fwd);
-            const bool obj = (kv != kNoKey) && (cls == kWallInner ? beats_wall(ax, ay, dx, dy, oz) : cls == kWallNone);
+            const bool obj = (kv != Key<K>::none) && (cls == kWallInner ? beats_wall(ax, ay, dx, dy, oz) : cls == kWallNone);
             nxt.sem[r * kSensor + k] = (int8_t)(obj ? (order < kOrderAgent ? 6 : species_[base + order - kOrderAgent])
                                                     : (cls == kWallNone ? -1 : 5));
             if (fixd)
@@ -505,10 +508,11 @@ void Sim::sensor_world(uint32_t w, Table &nxt)
                                                       : cls == kWallInner ? wall_z(ax, ay, dx, dy)
                                                       : cls == kWallBox ? np[k].c : __builtin_inff());
         }
-        const uint32_t kv = key[kSensor], order = kv & kOrderMask;
+        const K kv = key[kSensor];
+        const uint32_t order = Key<K>::order(kv);
         const int fcls = cls_of(kSensor, true);
-        const bool agent = kv != kNoKey && order >= kOrderAgent &&
-                           (fcls == kWallInner ? beats_wall(ax, ay, h.x, h.y, u2f(kv & ~kOrderMask)) : fcls == kWallNone);
+        const bool agent = kv != Key<K>::none && order >= kOrderAgent &&
+                           (fcls == kWallInner ? beats_wall(ax, ay, h.x, h.y, Key<K>::z(kv)) : fcls == kWallNone);
         finder_[base + i] = agent ? (int32_t)(order - kOrderAgent) : -1;
     }
 }

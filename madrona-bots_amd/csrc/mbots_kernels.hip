@@ -24,6 +24,7 @@
 #include "mbots_kernels.hpp"
 #include <stdlib.h>
 #include <algorithm>
+#include <type_traits>
 #include "mbots_ray.hpp"
 
 namespace mbots {
@@ -206,6 +207,12 @@ __device__ void world_step(SimState &S, const ObsTable &cur, WorldLDS<kCap> &L, 
 #define MB_K1_WPB 8   // 4: K1 +2.5 %, and +7 % step at 4096 worlds; 16: +30 % K1
 #endif
 constexpr int kK1Worlds = MB_K1_WPB;          // worlds (waves) per K1 block
+// per capacity class: the 512 / 1024-slot images (17 / 34 KB of LDS a world)
+// take 4 / 2 worlds a block, two blocks per CU
+template <int kCap>
+constexpr int k1_worlds() { return kCap <= 256 ? kK1Worlds : kCap == 512 ? 4 : 2; }
+template <int kCap>
+constexpr int k1_min_blocks() { return kCap <= 128 ? 32 / kK1Worlds : kCap <= 256 ? 16 / kK1Worlds : kCap == 512 ? 2 : 1; }
 // SGPRs capped at 80: the compiler's own choice (99, no spill at 80) admits only
 // 6 waves per SIMD (800 SGPRs per SIMD in 16-register granules plus 16), one
 // block in four fewer: K1 87 -> 78 us, step -1.7 %
@@ -213,21 +220,22 @@ constexpr int kK1Worlds = MB_K1_WPB;          // worlds (waves) per K1 block
 // instead of read from the last step's sensor, so K1 need not wait for it
 // (small world counts, where the step is a latency chain)
 template <int kCap, bool kFinder>
-__global__ __launch_bounds__(64 * kK1Worlds, (kCap <= 128 ? 32 : 16) / kK1Worlds)
+__global__ __launch_bounds__(64 * k1_worlds<kCap>(), k1_min_blocks<kCap>())
 __attribute__((amdgpu_num_sgpr(80))) void world_step_kernel(
     SimState S, ObsTable cur, int parity)
 {
-    __shared__ WorldLDS<kCap> lds[kK1Worlds];
-    __shared__ FinderScratch<kCap> fsc[kFinder ? kK1Worlds : 1];
+    constexpr int kW1 = k1_worlds<kCap>();
+    __shared__ WorldLDS<kCap> lds[kW1];
+    __shared__ FinderScratch<kCap> fsc[kFinder ? kW1 : 1];
     const uint32_t wv = threadIdx.x >> 6;
     const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t w = uniform(blockIdx.x * kK1Worlds + wv);
+    const uint32_t w = uniform(blockIdx.x * kW1 + wv);
     if (w < S.W) world_step<kCap, kFinder>(S, cur, lds[wv], fsc[kFinder ? wv : 0], w, lane);
     // counter-major tile buckets: [counter][tile][bucket] (K2 reads one
     // counter's buckets as contiguous 16-B words)
     const size_t nent = (size_t)S.ntiles * kTileBuckets;
     int32_t *tiles = S.tiles + (size_t)parity * 5 * nent;
-    if constexpr (kK1Worlds == 1) {
+    if constexpr (kW1 == 1) {
         // one world per block: its species/agent counts go straight to the K2
         // scan tile (no block barrier: a block's LDS frees as its world ends)
         if (w < S.Wx && lane < 5) {   // (a shard ghost, w >= Wx, is not counted)
@@ -236,7 +244,7 @@ __attribute__((amdgpu_num_sgpr(80))) void world_step_kernel(
                       lane < 4 ? sc[lane] : sc[0] + sc[1] + sc[2] + sc[3]);
         }
     } else {
-        __shared__ int32_t blk[kK1Worlds][5];
+        __shared__ int32_t blk[kW1][5];
         // per-block species/agent counts -> the K2 scan tile (one atomic per counter)
         if (lane < 5) {   // (a shard ghost, w >= Wx, is not counted: its rows follow the table's)
             const int32_t *sc = lds[wv].scount;
@@ -246,8 +254,8 @@ __attribute__((amdgpu_num_sgpr(80))) void world_step_kernel(
         if (threadIdx.x < 5) {
             int32_t v = 0;
 #pragma unroll
-            for (int k = 0; k < kK1Worlds; ++k) v += blk[k][threadIdx.x];
-            const uint32_t tile = (blockIdx.x * kK1Worlds) / kTileWorlds;
+            for (int k = 0; k < kW1; ++k) v += blk[k][threadIdx.x];
+            const uint32_t tile = (blockIdx.x * kW1) / kTileWorlds;
             atomicAdd(&tiles[threadIdx.x * nent + tile * kTileBuckets + blockIdx.x % kTileBuckets], v);
         }
     }
@@ -1298,7 +1306,10 @@ struct SensorLDS {
     float2 hd[kCap];                          // agent headings
     int8_t sem_of[kOrderAgent + kCap];        // semantic byte by object order: food 6,
                                               // agent 64 + slot its species
-    alignas(16) uint32_t key[kKeyAgents * kKeyStride];
+    // 32-bit keys up to 256 slots (orders < 320 fit the low 9 bits), 64-bit
+    // above (mbots_ray.hpp Key<>)
+    using key_t = std::conditional_t<(kCap <= 256), uint32_t, uint64_t>;
+    alignas(16) key_t key[kKeyAgents * kKeyStride];
     uint32_t qcode[kQueueCap + 1];            // P1 survivors: agent | object << 11 (+ a
                                               // sink slot for the branch-free write); a
                                               // survivor batch's wide pairs are compacted
@@ -1377,6 +1388,7 @@ template <class LDS>
 __device__ __forceinline__ void run_wide(LDS &L, const RayTab &R, int na, int a0, int q0, int cnt, uint32_t &mbc)
 {
     MB_CNT(6, (cnt + 1) / 2);
+    using K = typename LDS::key_t;
     const int lane = (int)__lane_id();
     // ray k's offset and near point (the near sphere): loop invariant
     const int k = lane & 31;
@@ -1398,14 +1410,14 @@ __device__ __forceinline__ void run_wide(LDS &L, const RayTab &R, int na, int a0
             const float us = R.u[ks];
             const NearPt nps{R.c[ks], R.s[ks], R.e[ks]};
             const bool fw = (ks < 24) | (ks == kSensor);
-            uint32_t kv;
+            K kv;
             if (j < na) {
                 const FoodBox b = box_setup(f, l, L.frot[j], L.hd[a0 + ic]);
-                kv = box_hit(b, us, fw, nps.c) ? zkey(box_z(b, fw), order) : kNoKey;
+                kv = box_hit(b, us, fw, nps.c) ? Key<K>::make(box_z(b, fw), order) : Key<K>::none;
             } else {
-                kv = pixel_key(f, l, us, nps, fw, order);
+                kv = pixel_key<K>(f, l, us, nps, fw, order);
             }
-            if (kv != kNoKey) atomicMin(&L.key[ic * kKeyStride + ks], kv);
+            if (kv != Key<K>::none) atomicMin(&L.key[ic * kKeyStride + ks], kv);
         }
     }
     for (int e0 = 0; e0 < cnt2; e0 += 2) {
@@ -1416,18 +1428,18 @@ __device__ __forceinline__ void run_wide(LDS &L, const RayTab &R, int na, int a0
             float f, l;
             uint32_t order;
             pair_fl(L, na, a0 + ic, j, f, l, order);
-            uint32_t *kr = L.key + ic * kKeyStride;
-            uint32_t kv, kf;
+            K *kr = L.key + ic * kKeyStride;
+            K kv, kf;
             if (j < na) {   // food square: every ray exactly
                 const FoodBox b = box_setup(f, l, L.frot[j], L.hd[a0 + ic]);
-                kv = box_hit(b, uk, k < 24, np.c) ? zkey(box_z(b, k < 24), order) : kNoKey;
-                kf = box_hit(b, 0.0f, true, fnp.c) ? zkey(box_z(b, true), order) : kNoKey;
+                kv = box_hit(b, uk, k < 24, np.c) ? Key<K>::make(box_z(b, k < 24), order) : Key<K>::none;
+                kf = box_hit(b, 0.0f, true, fnp.c) ? Key<K>::make(box_z(b, true), order) : Key<K>::none;
             } else {
-                kv = pixel_key(f, l, uk, np, k < 24, order);
-                kf = finder_key(f, l, order);
+                kv = pixel_key<K>(f, l, uk, np, k < 24, order);
+                kf = finder_key<K>(f, l, order);
             }
-            if (kv != kNoKey) atomicMin(&kr[k], kv);
-            if ((k == 0) & (kf != kNoKey)) atomicMin(&kr[kSensor], kf);
+            if (kv != Key<K>::none) atomicMin(&kr[k], kv);
+            if ((k == 0) & (kf != Key<K>::none)) atomicMin(&kr[kSensor], kf);
         }
     }
 }
@@ -1440,6 +1452,7 @@ __device__ __forceinline__ void run_survivors(LDS &L, const RayTab &R, int na, i
 {
     MB_CNT(3, 1);
     MB_CNT(4, cnt);
+    using K = typename LDS::key_t;
 #ifdef MB_COUNT
     int mb_t = 0;
     bool mb_food = false, mb_disc = false;
@@ -1501,7 +1514,7 @@ __device__ __forceinline__ void run_survivors(LDS &L, const RayTab &R, int na, i
             const int k1 = min((int)floorf(hi), kmax);
             const int c = k1 - k0 + 1;
             k0 += fwd ? 0 : 24;
-            uint32_t *kr = L.key + ic * kKeyStride;
+            K *kr = L.key + ic * kKeyStride;
             // The two edge pixels of [k0, k0 + c) get the exact predicate.
             // Interior pixels lie >= one pixel pitch minus 2 kUEps (>= 0.08 in
             // u) inside the true interval, where the approximate bounds are off
@@ -1513,18 +1526,18 @@ __device__ __forceinline__ void run_survivors(LDS &L, const RayTab &R, int na, i
             const int kl = k0 + max(c - 1, 0);
             const float ua = R.u[k0 & 31], ub = R.u[kl & 31];
             bool ha, hb, hf;
-            uint32_t kin;
+            K kin;
             if (food) {   // a far square: box_hit is the line test on its side
                 ha = box_line_hit(b, ua);
                 hb = box_line_hit(b, ub);
                 hf = fwd & box_finder_hit(b);
-                kin = zkey(box_z(b, fwd), order);
+                kin = Key<K>::make(box_z(b, fwd), order);
             } else {
                 ha = far_pixel_hit(f, l, ua, fwd);
                 hb = far_pixel_hit(f, l, ub, fwd);
                 // finder ray (u = 0) of a far pair: q(0) = l^2 - R^2 <= 0 and f > 0
                 hf = (l * l - kAgentR2 <= 0.0f) & fwd;
-                kin = zkey(fwd ? f - kAgentR : -f - kAgentR, order);
+                kin = Key<K>::make(fwd ? f - kAgentR : -f - kAgentR, order);
             }
             if ((c > 0) & ha) atomicMin(&kr[k0], kin);
             if ((c > 1) & hb) atomicMin(&kr[kl], kin);
@@ -1613,7 +1626,7 @@ constexpr int kSensorWorlds = MB_SENSOR_WPB;   // worlds (waves) per sensor bloc
 #endif
 // the launch bounds' minimum waves per SIMD: 8 (<= 64 VGPRs) for the 128-slot
 // class, 4 for the 256-slot one
-__host__ __device__ constexpr int sensor_min_waves(int cap) { return cap <= 128 ? 8 : 4; }
+__host__ __device__ constexpr int sensor_min_waves(int cap) { return cap <= 128 ? 8 : cap <= 256 ? 4 : 2; }
 // kDepth: fix_depth_alias (a depth byte per pixel besides the semantic one).
 // kSplit: kSplit waves share one world, each taking every kSplit-th key chunk
 // (each stages its own LDS image of the world).  Used at small world counts
@@ -1645,6 +1658,7 @@ __global__ __launch_bounds__(64 * kWaves, sensor_min_waves(kCap)) void sensor_ke
     const int kChunk0 = (int)(wv % kSplit) * kKeyAgents;
     if (w >= S.W) return;
     SensorLDS<kCap> &L = lds[wv];
+    using K = typename SensorLDS<kCap>::key_t;
     constexpr bool depth = kDepth;
     SensorPrefetch pf;
     sensor_prefetch(S, w, lane, pf);
@@ -1756,7 +1770,7 @@ __global__ __launch_bounds__(64 * kWaves, sensor_min_waves(kCap)) void sensor_ke
     for (int a0 = kChunk0; a0 < n; a0 += kChunkStep) {
         const int nc = min(kKeyAgents, n - a0);
         MB_CNT(1, 1);
-        for (int q = lane; q < nc * kKeyStride; q += 64) L.key[q] = kNoKey;
+        for (int q = lane; q < nc * kKeyStride; q += 64) L.key[q] = Key<K>::none;
         wave_sync();
         // ---- P1: wedge pre-cull of the chunk's (agent, object) pairs.  Lane =
         // (agent a, object group o): the chunk's nc agents rounded up to P = 1,
@@ -1897,7 +1911,15 @@ __global__ __launch_bounds__(64 * kWaves, sensor_min_waves(kCap)) void sensor_ke
             const int cc = min(ci, nc - 1);
             const int i = a0 + cc;
             const float2 p = L.obj[na + i], h = L.hd[i];
-            const uint4 kv4 = *reinterpret_cast<const uint4 *>(&L.key[cc * kKeyStride + 4 * g]);
+            K kvs[4];
+            if constexpr (sizeof(K) == 4) {
+                const uint4 kv4 = *reinterpret_cast<const uint4 *>(&L.key[cc * kKeyStride + 4 * g]);
+                kvs[0] = kv4.x; kvs[1] = kv4.y; kvs[2] = kv4.z; kvs[3] = kv4.w;
+            } else {
+                const ulonglong2 *kp = reinterpret_cast<const ulonglong2 *>(&L.key[cc * kKeyStride + 4 * g]);
+                const ulonglong2 k01 = kp[0], k23 = kp[1];
+                kvs[0] = k01.x; kvs[1] = k01.y; kvs[2] = k23.x; kvs[3] = k23.y;
+            }
             const float4 u4 = *reinterpret_cast<const float4 *>(&R.u[4 * g]);
             // the chunk's 64-slot group (8 | 64: one group per chunk), a uniform branch
             int r;
@@ -1914,7 +1936,6 @@ __global__ __launch_bounds__(64 * kWaves, sensor_min_waves(kCap)) void sensor_ke
             // rounding is sign-symmetric)
             const bool fw = g < 6;
             const float hxs = fw ? h.x : -h.x, hys = fw ? h.y : -h.y;
-            const uint32_t kvs[4] = {kv4.x, kv4.y, kv4.z, kv4.w};
             const float us[4] = {u4.x, u4.y, u4.z, u4.w};
             // every ray as if its near point lay in the inner rectangle (true
             // for every agent 1.2 inside it: the wall is the ray's exit) and
@@ -1926,10 +1947,10 @@ __global__ __launch_bounds__(64 * kWaves, sensor_min_waves(kCap)) void sensor_ke
             for (int t = 0; t < 4; ++t) {
                 const float u = us[t];
                 const float dx = hxs + u * hys, dy = hys + u * (-hxs);
-                const uint32_t kv = kvs[t];
-                const float oz = __uint_as_float(kv & ~kOrderMask);
-                const uint32_t order = kv & kOrderMask;
-                const bool obj = (kv != kNoKey) & beats_wall_in(lox, hix, loy, hiy, dx, dy, oz);
+                const K kv = kvs[t];
+                const float oz = Key<K>::z(kv);
+                const uint32_t order = Key<K>::order(kv);
+                const bool obj = (kv != Key<K>::none) & beats_wall_in(lox, hix, loy, hiy, dx, dy, oz);
                 // (read for any key: a miss's order bits 0x1FF clamp into the table)
                 const int sem = obj ? (int)L.sem_of[min(order, (uint32_t)(kOrderAgent + kCap - 1))] : 5;
                 semv |= (uint32_t)(uint8_t)(int8_t)sem << (8 * t);
@@ -1948,16 +1969,16 @@ __global__ __launch_bounds__(64 * kWaves, sensor_min_waves(kCap)) void sensor_ke
         if ((int)lane < nc) {
             const int i = a0 + (int)lane;
             const float2 p = L.obj[na + i], h = L.hd[i];
-            const uint32_t kv = L.key[lane * kKeyStride + kSensor];
-            const uint32_t order = kv & kOrderMask;
+            const K kv = L.key[lane * kKeyStride + kSensor];
+            const uint32_t order = Key<K>::order(kv);
 #ifndef MB_PROBE_ALL_DEEP   // (instruction-count probe: wrong rows near the walls)
             shallow = !((p.x >= kInLo + 1.2f) & (p.x <= kInHiX - 1.2f) & (p.y >= kInLo + 1.2f) &
                         (p.y <= kInHiY - 1.2f));
 #endif
             // (a shallow agent not strictly inside is redone below)
-            const bool agent = (kv != kNoKey) & (order >= kOrderAgent) &&
+            const bool agent = (kv != Key<K>::none) & (order >= kOrderAgent) &&
                                beats_wall_in(kInLo - p.x, kInHiX - p.x, kInLo - p.y, kInHiY - p.y, h.x, h.y,
-                                             __uint_as_float(kv & ~kOrderMask));
+                                             Key<K>::z(kv));
             S.finder[base + i] = agent ? (int32_t)(order - kOrderAgent) : -1;
         }
         // ---- the agents near the walls: each ray's near point
@@ -1991,14 +2012,14 @@ __global__ __launch_bounds__(64 * kWaves, sensor_min_waves(kCap)) void sensor_ke
                 const int cls = wall_class(fw ? p.x + ex : p.x - ex, fw ? p.y + ey : p.y - ey);
                 const bool edge = !strictly_inside(p.x, p.y);
                 if ((cls != kWallInner) | edge) {
-                    const uint32_t kv = L.key[ca * kKeyStride + k];
-                    const float oz = __uint_as_float(kv & ~kOrderMask);
-                    const uint32_t order = kv & kOrderMask;
+                    const K kv = L.key[ca * kKeyStride + k];
+                    const float oz = Key<K>::z(kv);
+                    const uint32_t order = Key<K>::order(kv);
                     const bool none = cls == kWallNone, inner = cls == kWallInner;
                     const float u = R.u[k];
                     const float hxs = fw ? h.x : -h.x, hys = fw ? h.y : -h.y;
                     const float dx = hxs + u * hys, dy = hys + u * (-hxs);
-                    const bool obj = (kv != kNoKey) & (none | (inner && beats_wall(p.x, p.y, dx, dy, oz)));
+                    const bool obj = (kv != Key<K>::none) & (none | (inner && beats_wall(p.x, p.y, dx, dy, oz)));
                     const int sem = obj ? (int)L.sem_of[min(order, (uint32_t)(kOrderAgent + kCap - 1))] : (none ? -1 : 5);
                     nxt.sem[(size_t)r * kSensor + k] = (int8_t)sem;
                     if (depth) {
@@ -2011,12 +2032,12 @@ __global__ __launch_bounds__(64 * kWaves, sensor_min_waves(kCap)) void sensor_ke
                     const float fx = fc * h.x + fsn * h.y, fy = fc * h.y + fsn * (-h.x);
                     const int fcls = wall_class(p.x + fx, p.y + fy);
                     if ((fcls != kWallInner) | edge) {
-                        const uint32_t kv = L.key[ca * kKeyStride + kSensor];
-                        const uint32_t order = kv & kOrderMask;
+                        const K kv = L.key[ca * kKeyStride + kSensor];
+                        const uint32_t order = Key<K>::order(kv);
                         const bool see = (fcls == kWallNone) |
                                          ((fcls == kWallInner) &&
-                                          beats_wall(p.x, p.y, h.x, h.y, __uint_as_float(kv & ~kOrderMask)));
-                        const bool agent = (kv != kNoKey) & (order >= kOrderAgent) & see;
+                                          beats_wall(p.x, p.y, h.x, h.y, Key<K>::z(kv)));
+                        const bool agent = (kv != Key<K>::none) & (order >= kOrderAgent) & see;
                         S.finder[base + i] = agent ? (int32_t)(order - kOrderAgent) : -1;
                     }
                 }
@@ -2628,13 +2649,20 @@ hipError_t launch_tile_sum(const SimState &S, int parity, hipStream_t st)
 }
 hipError_t launch_world_step(const SimState &S, const ObsTable &cur, int parity, hipStream_t st, hipEvent_t done)
 {
-    const dim3 grid((S.W + kK1Worlds - 1) / kK1Worlds), blk(64 * kK1Worlds);
-    auto go = [&](auto kern) {
+    auto go = [&](auto kern, int wpb) {
+        const dim3 grid((S.W + wpb - 1) / wpb), blk(64 * wpb);
         if (!done) hipLaunchKernelGGL(kern, grid, blk, 0, st, S, cur, parity);
         else hipExtLaunchKernelGGL(kern, grid, blk, 0u, st, nullptr, done, 0u, S, cur, parity);   // on the packet
     };
-    if (S.cap <= 128) S.k1_finder ? go(world_step_kernel<128, true>) : go(world_step_kernel<128, false>);
-    else S.k1_finder ? go(world_step_kernel<256, true>) : go(world_step_kernel<256, false>);
+    // (K1-finder mode is a <= 256-slot mode: its camera slots are bytes)
+    if (S.cap <= 128)
+        S.k1_finder ? go(world_step_kernel<128, true>, kK1Worlds) : go(world_step_kernel<128, false>, kK1Worlds);
+    else if (S.cap <= 256)
+        S.k1_finder ? go(world_step_kernel<256, true>, kK1Worlds) : go(world_step_kernel<256, false>, kK1Worlds);
+    else if (S.cap <= 512)
+        go(world_step_kernel<512, false>, k1_worlds<512>());
+    else
+        go(world_step_kernel<1024, false>, k1_worlds<1024>());
     return hipGetLastError();
 }
 hipError_t launch_scan(const SimState &S, int parity, hipStream_t st, hipEvent_t done, bool plain_events)
@@ -2747,7 +2775,14 @@ static void launch_sensor_cap(const SimState &S, const ObsTable &nxt, hipStream_
                               bool plain_events)
 {
     const bool fixd = (S.flags & kFlagFixDepth) != 0;
-    if (S.W <= (uint32_t)MB_SENSOR_SPLIT_MAX) {   // small: MB_SENSOR_SPLIT waves per world
+    if constexpr (kCap > 256) {
+        // the large classes (21 / 11 KB of LDS a world at 1024 / 512 slots):
+        // one wave per world, 1 / 2 worlds a block, no split
+        constexpr int kWv = kCap > 512 ? 1 : 2;
+        const dim3 grid((S.W + kWv - 1) / kWv), blk(64 * kWv);
+        if (fixd) MB_LAUNCH_EV((sensor_kernel<true, 1, kCap, kWv>), grid, blk, st, done, plain_events, S, nxt);
+        else MB_LAUNCH_EV((sensor_kernel<false, 1, kCap, kWv>), grid, blk, st, done, plain_events, S, nxt);
+    } else if (S.W <= (uint32_t)MB_SENSOR_SPLIT_MAX) {   // small: MB_SENSOR_SPLIT waves per world
         constexpr int kWv = MB_SENSOR_SPLIT_WAVES, kWpb = kWv / MB_SENSOR_SPLIT;
         const dim3 grid((S.W + kWpb - 1) / kWpb), blk(64 * kWv);
         if (fixd)
@@ -2766,7 +2801,9 @@ hipError_t launch_sensor(const SimState &S, const ObsTable &nxt, hipStream_t st,
                          bool plain_events)
 {
     if (S.cap <= 128) launch_sensor_cap<128>(S, nxt, st, done, plain_events);
-    else launch_sensor_cap<256>(S, nxt, st, done, plain_events);
+    else if (S.cap <= 256) launch_sensor_cap<256>(S, nxt, st, done, plain_events);
+    else if (S.cap <= 512) launch_sensor_cap<512>(S, nxt, st, done, plain_events);
+    else launch_sensor_cap<1024>(S, nxt, st, done, plain_events);
     return hipGetLastError();
 }
 hipError_t launch_shift(const SimState &S, const ObsTable &t, int mode, hipStream_t st)

@@ -767,7 +767,7 @@ int mbots_create(const mbots_config *cfg_in, mbots_handle **out)
         return fail(MBOTS_E_INVALID, "sensor_size must be 32 (mgr.hpp:19, entry.cpp:27)");
     static_assert(mbots::kMaxCap == (int)MBOTS_MAX_CAPACITY, "include/mbots.h");
     if (cfg.agent_capacity > (uint32_t)mbots::kMaxCap || cfg.agent_capacity < 4)
-        return fail(MBOTS_E_INVALID, "agent_capacity must be in [4, 256]");
+        return fail(MBOTS_E_INVALID, "agent_capacity must be in [4, " + std::to_string(mbots::kMaxCap) + "]");
     if (cfg.init_num_agents_per_world > cfg.agent_capacity)
         return fail(MBOTS_E_INVALID, "init_num_agents_per_world exceeds agent_capacity");
     if (cfg.init_num_agents_per_world < (uint32_t)mbots::kNumSpecies)
@@ -818,7 +818,8 @@ int mbots_create(const mbots_config *cfg_in, mbots_handle **out)
     S.world_offset = cfg.world_offset;
     S.flags = cfg.flags;
     S.seed = cfg.rand_seed;
-    h->k1_finder = S.W <= MB_K1_FINDER_MAX;
+    // (the K1 finder pass keeps camera slots in bytes: a <= 256-slot mode)
+    h->k1_finder = S.W <= MB_K1_FINDER_MAX && S.cap <= 256;
     S.k1_finder = h->k1_finder ? 1u : 0u;
 
     int rc = MBOTS_OK;
@@ -940,8 +941,9 @@ static int capacity_report(mbots_handle *h, uint32_t dropped)
             std::to_string(h->cfg.agent_capacity) + " (" + std::to_string(dropped) +
             " in total): the reference's worlds have no cap (sim.cpp:561-564, :830-834), so the run now "
             "differs from the reference's" +
-            (h->cfg.agent_capacity < MBOTS_MAX_CAPACITY ? std::string("; raise agent_capacity (at most 256)")
-                                                        : std::string(" (256 is the largest agent_capacity)"));
+            (h->cfg.agent_capacity < MBOTS_MAX_CAPACITY
+                 ? "; raise agent_capacity (at most " + std::to_string(MBOTS_MAX_CAPACITY) + ")"
+                 : " (" + std::to_string(MBOTS_MAX_CAPACITY) + " is the largest agent_capacity)");
     return (h->cfg.flags & MBOTS_FLAG_STRICT_CAPACITY) ? MBOTS_E_CAPACITY : MBOTS_W_CAPACITY;
 }
 

@@ -36,6 +36,31 @@ MB_HD uint32_t zkey(float z, uint32_t order)
     return (f2u(z) & ~kOrderMask) | order;
 }
 
+// Keys of the large capacity classes (512 / 1024 slots: agent orders past
+// 511 no longer fit the 9 low bits): the same quantised depth in the high
+// word, the order in the low one -- the same lexicographic (depth, order)
+// minimum as the 32-bit key wherever both can hold the order, so a world
+// renders the same bits in every class.  Key<K>: make / z / order / none.
+template <typename K>
+struct Key;
+template <>
+struct Key<uint32_t> {
+    static constexpr uint32_t none = kNoKey;
+    MB_HD static uint32_t make(float z, uint32_t order) { return zkey(z, order); }
+    MB_HD static float z(uint32_t k) { return u2f(k & ~kOrderMask); }
+    MB_HD static uint32_t order(uint32_t k) { return k & kOrderMask; }
+};
+template <>
+struct Key<uint64_t> {
+    static constexpr uint64_t none = ~0ull;
+    MB_HD static uint64_t make(float z, uint32_t order)
+    {
+        return ((uint64_t)(f2u(z) & ~kOrderMask) << 32) | order;
+    }
+    MB_HD static float z(uint64_t k) { return u2f((uint32_t)(k >> 32)); }
+    MB_HD static uint32_t order(uint64_t k) { return (uint32_t)k; }
+};
+
 // ray k's near point in the agent frame, (c, s) = 1.1 (1, u) / sqrt(1 + u^2)
 // (c is also the ray parameter s0 of that point along (1, u)), and
 // e = 1.1 sqrt(1 + u^2); the oracle's near_pt
@@ -124,7 +149,8 @@ MB_HD uint32_t order_of(int nf, int j)
 // (A = f^2 - R^2, C = l^2 - R^2); the ray leaves it beyond the near sphere iff
 // the near point lies inside it or the chord's midpoint lies beyond the near
 // point (+-p >= e, p = f + u l).  Key (depth f - R, backward -f - R) or kNoKey.
-MB_HD uint32_t pixel_key(float f, float l, float u, const NearPt &np, bool fwdk, uint32_t order)
+template <typename K = uint32_t>
+MB_HD K pixel_key(float f, float l, float u, const NearPt &np, bool fwdk, uint32_t order)
 {
     const float A = f * f - kAgentR2, B2 = 2.0f * (l * f), C = l * l - kAgentR2;
     const float q = (A * u - B2) * u + C;
@@ -132,8 +158,8 @@ MB_HD uint32_t pixel_key(float f, float l, float u, const NearPt &np, bool fwdk,
     const float nx = fwdk ? np.c - f : -np.c - f, ny = fwdk ? np.s - l : -np.s - l;
     const bool in0 = nx * nx + ny * ny <= kAgentR2;
     const bool hit = in0 | ((q <= 0.0f) & ((fwdk ? p : -p) >= np.e));
-    const uint32_t key = zkey(zq(max0(fwdk ? f - kAgentR : -f - kAgentR)), order);
-    return hit ? key : kNoKey;
+    const K key = Key<K>::make(zq(max0(fwdk ? f - kAgentR : -f - kAgentR)), order);
+    return hit ? key : Key<K>::none;
 }
 
 // pixel_key's hit test for a far pair (|f| > kCircleFar: the circle lies
@@ -151,9 +177,10 @@ MB_HD bool far_pixel_hit(float f, float l, float u, bool fwdk)
 // the finder ray (u = 0, forward; near point (1.1, 0), e = 1.1): pixel_key's
 // expressions at u = 0 (the oracle evaluates the generic form there)
 MB_HD NearPt finder_np() { return near_pt(0.0f); }
-MB_HD uint32_t finder_key(float f, float l, uint32_t order)
+template <typename K = uint32_t>
+MB_HD K finder_key(float f, float l, uint32_t order)
 {
-    return pixel_key(f, l, 0.0f, finder_np(), true, order);
+    return pixel_key<K>(f, l, 0.0f, finder_np(), true, order);
 }
 
 // ---------------------------------------------------------------------------

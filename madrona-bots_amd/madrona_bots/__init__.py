@@ -114,7 +114,7 @@ def _check(rc):
 
 
 _W_CAPACITY, _E_CAPACITY = 1, -5   # include/mbots.h MBOTS_W_CAPACITY / MBOTS_E_CAPACITY
-MAX_CAPACITY = 256                 # MBOTS_MAX_CAPACITY
+MAX_CAPACITY = 1024                # MBOTS_MAX_CAPACITY
 
 
 class CapacityWarning(RuntimeWarning):
@@ -371,7 +371,7 @@ class SimManager:
     SURVEY B.1), shard_ghost (also step world world_offset + num_worlds, never
     exported, so a shard's faithful B.3 rewards equal one device's; its agents
     act on the write_synthetic_actions stream), strict_capacity (a world that
-    reaches agent_capacity -- at most MAX_CAPACITY = 256 slots -- and drops a
+    reaches agent_capacity -- at most MAX_CAPACITY = 1024 slots -- and drops a
     birth or respawn makes step() raise CapacityError instead of warning with
     CapacityWarning: the reference has no cap)."""
 

@@ -160,12 +160,27 @@ def test_breed_heavy_to_capacity_256():
     W = 16
     mgr = _mgr(W, agent_capacity=256)
     orc = pyoracle.OracleSim(W, 69, 32, cap=256, num_threads=4)
-    with pytest.warns(mb.CapacityWarning, match="256 is the largest"):
+    with pytest.warns(mb.CapacityWarning, match="at most 1024"):
         _breed_steps(mgr, orc, 40)
     assert mgr.overflow() == orc.overflow() > 0
 
 
+@pytest.mark.parametrize("cap,W,steps", [(512, 16, 70), (1024, 8, 110)])
+def test_breed_heavy_large_capacity_classes(cap, W, steps):
+    """The 512- and 1024-slot classes (64-bit sensor keys: agent orders past
+    511) under the breed-heavy stream until the cap binds: every column and
+    the dropped-birth count equal the oracle's."""
+    import madrona_bots as mb
+    mgr = _mgr(W, agent_capacity=cap)
+    orc = pyoracle.OracleSim(W, 69, 32, cap=cap, num_threads=4)
+    with pytest.warns(mb.CapacityWarning):
+        peak = _breed_steps(mgr, orc, steps)
+    assert peak == cap
+    assert mgr.overflow() == orc.overflow() > 0
+
+
 def _breed_steps(mgr, orc, steps):
+    peak = 0
     for t in range(steps):
         g = torch.Generator().manual_seed(1000 + t)
         n = mgr.num_agents()
@@ -183,6 +198,8 @@ def _breed_steps(mgr, orc, steps):
         assert not errs, errs[:5]
         mgr.shift_observations()
         orc.shift_observations()
+        peak = max(peak, int(mgr.species_count_tensor().to_torch().sum(1).max()))
+    return peak
 
 
 @pytest.mark.gpu

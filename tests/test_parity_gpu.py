@@ -445,17 +445,18 @@ def _breed_heavy(n, step):
     return a
 
 
-@pytest.mark.parametrize("cap", [256, 128])
-def test_capacity_classes_breed_heavy(cap):
-    """Worlds filling 128 and 256 slots (the two kernel capacity classes: four
-    64-slot groups in K1 and the sensor at 256) under a breed-heavy stream:
-    every column and the dropped-birth count equal the oracle's."""
+@pytest.mark.parametrize("cap,W,steps", [(256, 48, 45), (128, 48, 45), (512, 16, 70), (1024, 8, 110)])
+def test_capacity_classes_breed_heavy(cap, W, steps):
+    """Worlds filling each kernel capacity class under a breed-heavy stream --
+    128 and 256 slots (two / four 64-slot groups in K1 and the sensor), 512
+    and 1024 (4 / 2 worlds per K1 block, one wave per world in the sensor,
+    64-bit depth keys): every column and the dropped-birth count equal the
+    oracle's after every step."""
     import madrona_bots as mb
-    W = 48
     mgr = mb.SimManager(0, W, 69, 32, agent_capacity=cap)
     orc = pyoracle.OracleSim(W, 69, 32, cap=cap, num_threads=8)
     peak = 0
-    for t in range(45):
+    for t in range(steps):
         n = mgr.num_agents()
         a = _breed_heavy(n, t)
         mgr.action_tensor(False).to_torch().copy_(a.to("cuda"))
@@ -469,6 +470,27 @@ def test_capacity_classes_breed_heavy(cap):
         peak = max(peak, int(mgr.species_count_tensor().to_torch().sum(1).max()))
     assert mgr.overflow() == orc.overflow() > 0
     assert peak == cap
+
+
+@pytest.mark.parametrize("cap,W", [(512, 4100), (1024, 8192)])
+def test_large_capacity_classes_bench_stream(cap, W):
+    """The 512 / 1024-slot classes at world counts past the split sensor and
+    the K1 finder mode (4100: no population order; 8192: K2's population order
+    and the value-wait fork / join) on the bench's synthetic stream, against
+    the oracle after every step and shift."""
+    import madrona_bots as mb
+    mgr = mb.SimManager(0, W, 69, 32, agent_capacity=cap)
+    orc = pyoracle.OracleSim(W, 69, 32, cap=cap, num_threads=16)
+    for t in range(6):
+        for s in (mgr, orc):
+            s.write_synthetic_actions(1234, t, True)
+            s.step()
+        errs = compare(mgr, orc, f"step {t}")
+        assert not errs, errs[:5]
+        mgr.shift_observations()
+        orc.shift_observations()
+        errs = compare(mgr, orc, f"shift {t}")
+        assert not errs, errs[:5]
 
 
 @pytest.mark.parametrize("W", [64, 1024, 4100])
