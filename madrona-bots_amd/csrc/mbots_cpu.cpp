@@ -12,7 +12,9 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <string>
 #include <thread>
+#include <type_traits>
 
 namespace mbots {
 namespace cpu {
@@ -673,10 +675,13 @@ namespace {
 constexpr char kMagic[8] = {'M', 'B', 'O', 'T', 'S', 'C', 'P', 'U'};
 }  // namespace
 
-#define MB_CPU_ARRAYS(X)                                                                          \
+#define MB_CPU_SLOT_ARRAYS(X)                                                                     \
     X(x_) X(y_) X(rw_) X(rz_) X(sur0_) X(sur1_) X(species_) X(health_) X(finder_) X(obsrow_)       \
-    X(stats_) X(n_) X(cur_food_) X(scount_) X(row_base_) X(world_off_) X(key_) X(ctr_)            \
-    X(overflow_) X(food_rot_) X(food_) X(sreward_)
+    X(stats_)
+#define MB_CPU_WORLD_ARRAYS(X)                                                                    \
+    X(n_) X(cur_food_) X(scount_) X(row_base_) X(world_off_) X(key_) X(ctr_) X(overflow_)         \
+    X(food_rot_) X(food_) X(sreward_)
+#define MB_CPU_ARRAYS(X) MB_CPU_SLOT_ARRAYS(X) MB_CPU_WORLD_ARRAYS(X)
 #define MB_CPU_TABLE(X)                                                                           \
     X(species) X(health) X(action) X(stats) X(pspecies) X(phealth) X(paction) X(pstats) X(pos)     \
     X(sur) X(reward) X(hidden) X(ppos) X(psur) X(preward) X(phidden) X(sem) X(psem) X(depth)      \
@@ -717,28 +722,75 @@ int Sim::save(void *dst, uint64_t bytes, std::string &err) const
 
 int Sim::load(const void *src, uint64_t bytes, std::string &err)
 {
-    if (bytes != checkpoint_bytes()) { err = "checkpoint size mismatch"; return MBOTS_E_INVALID; }
+    if (bytes < sizeof(kMagic) + sizeof(mbots_config)) { err = "checkpoint truncated"; return MBOTS_E_INVALID; }
     const char *p = static_cast<const char *>(src);
     if (memcmp(p, kMagic, sizeof(kMagic)) != 0) { err = "not a CPU-mode checkpoint"; return MBOTS_E_INVALID; }
     mbots_config c;
     memcpy(&c, p + sizeof(kMagic), sizeof(c));
-    if (c.num_worlds != cfg_.num_worlds || c.agent_capacity != cfg_.agent_capacity ||
+    // (another agent_capacity is fine when every world of the blob fits this
+    // one's: the per-slot arrays are re-laid out world by world, the table's
+    // first N rows copied -- SimManager(agent_capacity="auto"))
+    if (c.num_worlds != cfg_.num_worlds || c.agent_capacity < 4 || c.agent_capacity > (uint32_t)kMaxCap ||
         c.init_num_agents_per_world != cfg_.init_num_agents_per_world ||
         c.world_offset != cfg_.world_offset || c.flags != cfg_.flags || c.rand_seed != cfg_.rand_seed) {
         err = "checkpoint configuration differs from the manager's";
         return MBOTS_E_INVALID;
+    }
+    const size_t cap_src = c.agent_capacity;
+    // bytes of array v in the blob: per-slot arrays and table columns scale
+    // with the capacity, per-world arrays do not
+    auto src_bytes = [&](size_t elems, size_t elem_bytes, bool per_slot) {
+        return (per_slot ? elems / cap_ * cap_src : elems) * elem_bytes;
+    };
+    size_t need = sizeof(kMagic) + sizeof(mbots_config) + sizeof(N_) + sizeof(totals_) + sizeof(agent_steps_);
+    size_t n_off = 0;
+#define X(v) need += src_bytes(v.size(), sizeof(v[0]), true);
+    MB_CPU_SLOT_ARRAYS(X)
+#undef X
+    n_off = need;
+#define X(v) need += src_bytes(v.size(), sizeof(v[0]), false);
+    MB_CPU_WORLD_ARRAYS(X)
+#undef X
+    const Table &t0 = T_[0];
+#define X(c) need += src_bytes(t0.c.size(), sizeof(t0.c[0]), true);
+    MB_CPU_TABLE(X)
+#undef X
+    if (bytes != need) { err = "checkpoint size mismatch"; return MBOTS_E_INVALID; }
+    for (uint32_t w = 0; w < W_; ++w) {   // n_ leads the per-world arrays
+        int32_t n;
+        memcpy(&n, p + n_off + 4 * (size_t)w, 4);
+        if (n < 0 || (size_t)n > cap_) {
+            err = "a world of the checkpoint holds " + std::to_string(n) + " agents, more than agent_capacity " +
+                  std::to_string(cap_);
+            return MBOTS_E_INVALID;
+        }
     }
     p += sizeof(kMagic) + sizeof(c);
     auto r = [&](void *d, size_t n) { memcpy(d, p, n); p += n; };
     r(&N_, sizeof(N_));
     r(totals_, sizeof(totals_));
     r(&agent_steps_, sizeof(agent_steps_));
+    auto slot = [&](auto &v) {   // [world][cap_src] -> [world][cap_]
+        using E = std::remove_reference_t<decltype(v[0])>;
+        const size_t keep = std::min(cap_src, (size_t)cap_);
+        for (size_t w = 0; w < v.size() / cap_; ++w) memcpy(&v[w * cap_], p + w * cap_src * sizeof(E), keep * sizeof(E));
+        p += v.size() / cap_ * cap_src * sizeof(E);
+    };
+#define X(v) slot(v);
+    MB_CPU_SLOT_ARRAYS(X)
+#undef X
 #define X(v) r(v.data(), v.size() * sizeof(v[0]));
-    MB_CPU_ARRAYS(X)
+    MB_CPU_WORLD_ARRAYS(X)
 #undef X
     tb_ = 0;
     Table &t = T_[0];
-#define X(c) r(t.c.data(), t.c.size() * sizeof(t.c[0]));
+    auto col = [&](auto &v) {   // the first N rows live; the rest stale
+        using E = std::remove_reference_t<decltype(v[0])>;
+        const size_t sb = v.size() / cap_ * cap_src * sizeof(E);
+        memcpy(v.data(), p, std::min(sb, v.size() * sizeof(E)));
+        p += sb;
+    };
+#define X(c) col(t.c);
     MB_CPU_TABLE(X)
 #undef X
     return MBOTS_OK;

@@ -603,11 +603,14 @@ struct Seg {
     size_t bytes;
 };
 
-std::vector<Seg> ckpt_segments(mbots_handle *h, mbots::ObsTable &t, uint32_t n_rows)
+// the first kSlotSegs segments are per-slot columns ([world][cap]); `cap`:
+// the capacity the segments are sized for (0: the manager's)
+constexpr size_t kSlotSegs = 11;
+std::vector<Seg> ckpt_segments(mbots_handle *h, mbots::ObsTable &t, uint32_t n_rows, uint32_t cap = 0)
 {
     using namespace mbots;
     SimState &S = h->S;
-    const size_t W = S.W, rows = W * h->cfg.agent_capacity, N = n_rows;
+    const size_t W = S.W, rows = W * (cap ? cap : h->cfg.agent_capacity), N = n_rows;
     std::vector<Seg> v = {
         {S.x, rows * 4}, {S.y, rows * 4}, {S.rw, rows * 4}, {S.rz, rows * 4},
         {S.species, rows * 4}, {S.health, rows * 4}, {S.finder, rows * 4}, {S.obsrow, rows * 4},
@@ -1780,27 +1783,41 @@ int mbots_load_checkpoint(mbots_handle *h, const void *src, uint64_t bytes)
     memcpy(&hd, src, sizeof(hd));
     if (memcmp(hd.magic, "MBOTSCK", 8) != 0 || hd.version != kCkptVersion)
         return fail(MBOTS_E_INVALID, "not a checkpoint of this version");
-    if (hd.num_worlds != h->cfg.num_worlds || hd.cap != h->cfg.agent_capacity ||
+    // (another agent_capacity is fine when every world of the blob fits this
+    // manager's: its per-slot columns are re-laid out, world by world -- a
+    // learner growing its worlds' capacity, SimManager(agent_capacity="auto"))
+    if (hd.num_worlds != h->cfg.num_worlds || hd.cap < 4 || hd.cap > (uint32_t)mbots::kMaxCap ||
         hd.A != h->cfg.init_num_agents_per_world || hd.world_offset != h->cfg.world_offset ||
         hd.flags != h->cfg.flags || hd.seed != h->cfg.rand_seed)
         return fail(MBOTS_E_INVALID, "checkpoint configuration differs from the manager's");
-    if (hd.n_rows > (uint64_t)h->S.W * h->cfg.agent_capacity)
+    const uint32_t cap = h->cfg.agent_capacity, cap_src = hd.cap;
+    if (hd.n_rows > (uint64_t)h->S.W * cap)
         return fail(MBOTS_E_INVALID, "checkpoint row count out of range");
     if (int rc = capture_guard(h, h->last_stream)) return rc;
     const auto segs = ckpt_segments(h, h->T[0], hd.n_rows);
-    if (bytes < ckpt_bytes(segs) || hd.bytes != ckpt_bytes(segs))
+    const auto segs_src = ckpt_segments(h, h->T[0], hd.n_rows, cap_src);
+    if (bytes < ckpt_bytes(segs_src) || hd.bytes != ckpt_bytes(segs_src))
         return fail(MBOTS_E_INVALID, "checkpoint size mismatch");
     {
         // the blob's own totals must agree with its header before anything is
-        // overwritten (a mismatch used to leave the manager half restored)
+        // overwritten (a mismatch used to leave the manager half
+        // restored), and every world's population must fit this capacity
         const char *q = static_cast<const char *>(src) + sizeof(hd);
-        for (const Seg &s : segs) {
+        for (const Seg &s : segs_src) {
             if (s.p == h->S.totals) {
                 uint32_t tot[8];
                 memcpy(tot, q, sizeof(tot));
                 if (tot[mbots::kTotRows] != hd.n_rows || tot[0] > hd.n_rows)
                     return fail(MBOTS_E_INVALID, "checkpoint row count disagrees with its saved totals");
-                break;
+            }
+            if (s.p == h->S.n) {
+                for (size_t w = 0; w < h->S.W; ++w) {
+                    int32_t n;
+                    memcpy(&n, q + 4 * w, 4);
+                    if (n < 0 || (uint32_t)n > cap)
+                        return fail(MBOTS_E_INVALID, "a world of the checkpoint holds " + std::to_string(n) +
+                                                         " agents, more than agent_capacity " + std::to_string(cap));
+                }
             }
             q += s.bytes;
         }
@@ -1808,9 +1825,15 @@ int mbots_load_checkpoint(mbots_handle *h, const void *src, uint64_t bytes)
     HIP_TRY(hipSetDevice(h->device));
     HIP_TRY(hipDeviceSynchronize());
     const char *p = static_cast<const char *>(src) + sizeof(hd);
-    for (const Seg &s : segs) {
-        if (s.bytes) HIP_TRY(hipMemcpy(s.p, p, s.bytes, hipMemcpyHostToDevice));
-        p += s.bytes;
+    for (size_t i = 0; i < segs.size(); ++i) {
+        const Seg &s = segs[i];
+        if (i < kSlotSegs && cap != cap_src) {   // [world][cap_src] -> [world][cap]
+            HIP_TRY(hipMemcpy2D(s.p, (size_t)cap * 4, p, (size_t)cap_src * 4, (size_t)std::min(cap, cap_src) * 4,
+                                h->S.W, hipMemcpyHostToDevice));
+        } else if (s.bytes) {
+            HIP_TRY(hipMemcpy(s.p, p, s.bytes, hipMemcpyHostToDevice));
+        }
+        p += segs_src[i].bytes;
     }
     HIP_TRY(hipMemset(h->S.tiles, 0, (size_t)2 * h->S.ntiles * mbots::kTileBuckets * 5 * sizeof(int32_t)));
     h->tb = 0;

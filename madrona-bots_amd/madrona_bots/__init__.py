@@ -26,7 +26,8 @@ import warnings
 import torch  # loads the HIP runtime libmbots.so links against (same soname)
 
 __all__ = ["SimManager", "ScriptBotsViewer", "Tensor", "madrona", "ExportID", "ExecMode", "unpack_rollout",
-           "unpack_learner", "rebuild_learner", "CapacityWarning", "CapacityError", "MAX_CAPACITY"]
+           "unpack_learner", "rebuild_learner", "CapacityWarning", "CapacityError", "MAX_CAPACITY",
+           "CAPACITY_CLASSES"]
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB_PATH = os.path.join(_HERE, "libmbots.so")
@@ -115,6 +116,16 @@ def _check(rc):
 
 _W_CAPACITY, _E_CAPACITY = 1, -5   # include/mbots.h MBOTS_W_CAPACITY / MBOTS_E_CAPACITY
 MAX_CAPACITY = 1024                # MBOTS_MAX_CAPACITY
+CAPACITY_CLASSES = (128, 256, 512, 1024)   # the kernels' slot classes
+
+
+def _capacity_class(need):
+    """The smallest kernel capacity class holding `need` agents (the largest
+    class when none does)."""
+    for c in CAPACITY_CLASSES:
+        if need <= c:
+            return c
+    return MAX_CAPACITY
 
 
 class CapacityWarning(RuntimeWarning):
@@ -373,7 +384,17 @@ class SimManager:
     act on the write_synthetic_actions stream), strict_capacity (a world that
     reaches agent_capacity -- at most MAX_CAPACITY = 1024 slots -- and drops a
     birth or respawn makes step() raise CapacityError instead of warning with
-    CapacityWarning: the reference has no cap)."""
+    CapacityWarning: the reference has no cap).
+
+    agent_capacity="auto" grows the worlds' capacity instead of dropping
+    agents: before each step() the manager reads the largest world population
+    n (one synchronisation) and, when the step could overflow -- a step adds at
+    most n births (one per agent, sim.cpp:561-564) and A respawns
+    (:830-834) -- moves its state into the next capacity class (128, 256, 512,
+    1024) through a checkpoint, so the run stays the reference's (bitwise equal
+    to a manager that never drops) up to 1024 agents per world.  Views fetched
+    before a growth keep the old storage alive but no longer follow the
+    manager: take them after step(), as learn/training_loop.py:43-50 does."""
 
     def __init__(self, gpu_id, num_worlds, rand_seed, init_num_agents_per_world, *,
                  exec_mode="hip", agent_capacity=128, world_offset=0, reward_fixed=False,
@@ -381,22 +402,56 @@ class SimManager:
         self.exec_mode = _exec_mode(exec_mode)
         self.gpu_id = int(gpu_id)
         self.num_worlds = int(num_worlds)
+        self._auto_cap = isinstance(agent_capacity, str)
+        if self._auto_cap:
+            if agent_capacity != "auto":
+                raise ValueError('agent_capacity must be an int or "auto"')
+            if shard_ghost:
+                raise ValueError('agent_capacity="auto" does not combine with shard_ghost')
+            agent_capacity = _capacity_class(3 * int(init_num_agents_per_world))
         self.agent_capacity = int(agent_capacity)
         flags = (FLAG_REWARD_FIXED if reward_fixed else 0) | \
                 (FLAG_FIX_DEPTH_ALIAS if fix_depth_alias else 0) | \
                 (FLAG_SHARD_GHOST if shard_ghost else 0) | \
                 (FLAG_STRICT_CAPACITY if strict_capacity else 0)
-        cfg = _Config(self.gpu_id, self.num_worlds, int(rand_seed) & 0xFFFFFFFF,
-                      int(init_num_agents_per_world), 32, int(world_offset),
-                      int(agent_capacity), flags, self.exec_mode)
+        self._cfg = (self.gpu_id, self.num_worlds, int(rand_seed) & 0xFFFFFFFF,
+                     int(init_num_agents_per_world), 32, int(world_offset), flags, self.exec_mode)
+        self._ghost = bool(shard_ghost)
+        self._fix_depth = bool(fix_depth_alias)
+        self._ktiming = False
+        self._open(self.agent_capacity)
+
+    def _open(self, cap):
+        """Create the native manager at capacity `cap` (and reset the caches
+        that belong to one)."""
+        g, W, seed, A, sensor, off, flags, mode = self._cfg
+        cfg = _Config(g, W, seed, A, sensor, off, int(cap), flags, mode)
         h = ctypes.c_void_p()
         _check(_lib.mbots_create(ctypes.byref(cfg), ctypes.byref(h)))
         self._hd = _Handle(h)        # destroyed when the manager and all its views are gone
         self._h = h
+        self.agent_capacity = int(cap)
         # row slots of every table column (the shard ghost is one more world)
-        self._cap_rows = (self.num_worlds + (1 if shard_ghost else 0)) * self.agent_capacity
-        self._fix_depth = bool(fix_depth_alias)
+        self._cap_rows = (self.num_worlds + (1 if self._ghost else 0)) * self.agent_capacity
         self._views = {}
+
+    def _grow_if_needed(self):
+        """agent_capacity="auto": the next capacity class before a step that
+        could overflow this one (at most 2 n + A agents after it)."""
+        if self.agent_capacity >= MAX_CAPACITY:
+            return
+        sc = self.species_count_tensor().to_torch()
+        n = int(sc.sum(dim=1).max()) if sc.numel() else 0
+        need = 2 * n + self._cfg[3]
+        if need <= self.agent_capacity:
+            return
+        blob = self.save_checkpoint()
+        old = self._hd
+        self._open(_capacity_class(need))
+        _check(_lib.mbots_load_checkpoint(self._h, ctypes.c_void_p(blob.ctypes.data), blob.size))
+        if self._ktiming:
+            self.enable_kernel_timing(True)
+        del old                      # (freed now unless a view still holds it)
 
     def _stream(self):
         if self.exec_mode == ExecMode.CPU:
@@ -432,6 +487,8 @@ class SimManager:
 
     # -- graphs -------------------------------------------------------------
     def step(self):
+        if self._auto_cap:
+            self._grow_if_needed()
         rc = _lib.mbots_step(self._h, self._stream())
         if rc == _W_CAPACITY:   # the step ran; agents were dropped at the cap (reported late by a few steps)
             warnings.warn(f"madrona_bots: {_lib.mbots_last_error().decode(errors='replace')}",
@@ -701,6 +758,7 @@ class SimManager:
         return v.value
 
     def enable_kernel_timing(self, enable=True):
+        self._ktiming = bool(enable)
         _check(_lib.mbots_enable_kernel_timing(self._h, 1 if enable else 0))
 
     def schedule_info(self):

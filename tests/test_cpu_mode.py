@@ -179,9 +179,55 @@ def test_breed_heavy_large_capacity_classes(cap, W, steps):
     assert mgr.overflow() == orc.overflow() > 0
 
 
-def _breed_steps(mgr, orc, steps):
+def test_auto_capacity_grows_without_drops():
+    """agent_capacity="auto": the breed-heavy stream grows the worlds through
+    the capacity classes (the state moved by a cross-capacity checkpoint before
+    each step that could overflow) and every column stays bitwise equal to an
+    oracle that never drops an agent -- the reference's unbounded tables, up to
+    1024 per world."""
+    import madrona_bots as mb
+    W = 8
+    mgr = _mgr(W, agent_capacity="auto")
+    orc = pyoracle.OracleSim(W, 69, 32, cap=1024, num_threads=4)
+    assert mgr.agent_capacity == 128
+    seen = {mgr.agent_capacity}
     peak = 0
-    for t in range(steps):
+    for t in range(80):
+        peak = max(peak, _breed_steps(mgr, orc, 1, t0=t))
+        seen.add(mgr.agent_capacity)
+    assert {128, 256, 512} <= seen and peak > 256
+    assert mgr.overflow() == orc.overflow() == 0
+
+
+def test_checkpoint_across_capacities():
+    """A checkpoint restores into a manager of another capacity when every
+    world fits (the per-slot columns re-laid out); a world that does not fit
+    is refused before anything is overwritten."""
+    a = _mgr(16, agent_capacity=128)
+    for t in range(6):
+        a.write_synthetic_actions(1234, t, True)
+        a.step()
+        a.shift_observations()
+    blob = a.save_checkpoint()
+    for cap in (512, 64):
+        b = _mgr(16, agent_capacity=cap)
+        b.load_checkpoint(blob.tobytes())
+        for t in range(6, 10):
+            for m in (a, b) if cap == 512 else (b,):
+                m.write_synthetic_actions(1234, t, True)
+                m.step()
+                m.shift_observations()
+        if cap == 512:
+            for name in ("position_tensor", "reward_tensor", "semantic_tensor", "hidden_state_tensor"):
+                for prev in (False, True):
+                    assert torch.equal(getattr(a, name)(prev).to_torch(), getattr(b, name)(prev).to_torch())
+    with pytest.raises(RuntimeError, match="more than agent_capacity"):
+        _mgr(16, agent_capacity=32).load_checkpoint(blob.tobytes())
+
+
+def _breed_steps(mgr, orc, steps, t0=0):
+    peak = 0
+    for t in range(t0, t0 + steps):
         g = torch.Generator().manual_seed(1000 + t)
         n = mgr.num_agents()
         r = torch.randint(0, 8, (n,), generator=g)

@@ -472,6 +472,61 @@ def test_capacity_classes_breed_heavy(cap, W, steps):
     assert peak == cap
 
 
+@pytest.mark.parametrize("W,steps", [(8, 80), (2100, 30)])
+def test_auto_capacity_grows_without_drops(W, steps):
+    """agent_capacity="auto" on the device: the breed-heavy stream grows the
+    worlds through the capacity classes (cross-capacity checkpoint hand-overs
+    before each step that could overflow) and every column stays bitwise equal
+    to an oracle that never drops (cap 1024), after every step."""
+    import madrona_bots as mb
+    mgr = mb.SimManager(0, W, 69, 32, agent_capacity="auto")
+    orc = pyoracle.OracleSim(W, 69, 32, cap=1024, num_threads=16)
+    seen = {mgr.agent_capacity}
+    for t in range(steps):
+        n = mgr.num_agents()
+        a = _breed_heavy(n, t)
+        mgr.action_tensor(False).to_torch().copy_(a.to("cuda"))
+        orc.column(pyoracle.COL_ACTION)[:] = a.numpy()
+        mgr.step()
+        orc.step()
+        seen.add(mgr.agent_capacity)
+        errs = compare(mgr, orc, f"step {t} cap {mgr.agent_capacity}")
+        assert not errs, errs[:5]
+        mgr.shift_observations()
+        orc.shift_observations()
+    assert {128, 256} <= seen
+    assert mgr.overflow() == orc.overflow() == 0
+
+
+def test_checkpoint_across_capacities_gpu():
+    """A device checkpoint restores into managers of other capacity classes
+    (per-slot columns re-laid out world by world) and the runs continue
+    bitwise equal; a world that does not fit is refused."""
+    import madrona_bots as mb
+    a = mb.SimManager(0, 4100, 69, 32)
+    for t in range(6):
+        a.write_synthetic_actions(1234, t, True)
+        a.step()
+        a.shift_observations()
+    blob = a.save_checkpoint()
+    others = [mb.SimManager(0, 4100, 69, 32, agent_capacity=c) for c in (256, 1024)]
+    for b in others:
+        b.load_checkpoint(blob.tobytes())
+    for t in range(6, 10):
+        for m in [a] + others:
+            m.write_synthetic_actions(1234, t, True)
+            m.step()
+            m.shift_observations()
+    for b in others:
+        for name in ("position_tensor", "reward_tensor", "semantic_tensor", "hidden_state_tensor",
+                     "action_tensor", "stats_tensor"):
+            for prev in (False, True):
+                assert torch.equal(getattr(a, name)(prev).to_torch(), getattr(b, name)(prev).to_torch()), \
+                    (b.agent_capacity, name, prev)
+    with pytest.raises(RuntimeError, match="more than agent_capacity|row count out of range"):
+        mb.SimManager(0, 4100, 69, 32, agent_capacity=32).load_checkpoint(blob.tobytes())
+
+
 @pytest.mark.parametrize("cap,W", [(512, 4100), (1024, 8192)])
 def test_large_capacity_classes_bench_stream(cap, W):
     """The 512 / 1024-slot classes at world counts past the split sensor and
