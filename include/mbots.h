@@ -292,7 +292,11 @@ int mbots_num_rows(mbots_handle *h, uint32_t *out);
 /* Checkpoint / restore (the reference has none): the live state
  * after the last step (agent SoA, RNG keys/counters, food, the current export
  * table's N rows) as a host blob.  A manager created with the same
- * configuration continues bit-exactly after mbots_load_checkpoint. */
+ * configuration continues bit-exactly after mbots_load_checkpoint -- also
+ * one of another agent_capacity, when every world of the blob fits it (the
+ * per-slot columns are re-laid out; a world that does not fit is refused
+ * before anything is overwritten).  The Python SimManager's
+ * agent_capacity="auto" grows a run through the capacity classes this way. */
 int mbots_checkpoint_size(mbots_handle *h, uint64_t *bytes);
 int mbots_save_checkpoint(mbots_handle *h, void *host_dst, uint64_t bytes);
 int mbots_load_checkpoint(mbots_handle *h, const void *host_src, uint64_t bytes);
