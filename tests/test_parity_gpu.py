@@ -315,13 +315,16 @@ def test_random_call_sequences(seed, W=None):
     checkpoint hand-overs against the oracle.  Each read materialises one
     lazily shifted or deferred column at a different point of the step cycle,
     and construct_obs(prev) gathers the still-deferred Prev columns itself; a
-    checkpoint saved at any point of the cycle continues in a fresh manager.
+    checkpoint saved at any point of the cycle continues in a fresh manager of
+    a random capacity class (128 / 256 / 512 / 1024: the cross-capacity load
+    agent_capacity="auto" grows through).
     Small world counts run in K1-finder mode (no wait for the last sensor),
     4100 worlds on the joined schedule with its value waits.  A full
     comparison follows every few operations and at the end."""
     from simpair import COLUMNS, bits, gpu_column
     import madrona_bots as mb
     rng = np.random.default_rng(seed)
+    caps = np.random.default_rng(seed + 1000)   # (its own stream: the op sequences stay the seeds')
     W = W or (4100 if seed % 4 == 0 else 20 + seed)
     fixd = bool(seed % 2)
     mgr = mb.SimManager(0, W, 69, 32, fix_depth_alias=fixd)
@@ -332,7 +335,8 @@ def test_random_call_sequences(seed, W=None):
         if op == 7:
             if rng.integers(0, 2):   # (half the draws: a checkpoint is a rare call)
                 blob = mgr.save_checkpoint()
-                mgr = mb.SimManager(0, W, 69, 32, fix_depth_alias=fixd)
+                cap = int(caps.choice(mb.CAPACITY_CLASSES))
+                mgr = mb.SimManager(0, W, 69, 32, fix_depth_alias=fixd, agent_capacity=cap)
                 mgr.load_checkpoint(blob)
             continue
         if op in (0, 1):
