@@ -240,7 +240,10 @@ class Tensor:
         # the learner reads ~10 views per step and is host-bound at small world
         # counts (scripts/refhost.py); building a view from the array interface
         # every time is most of an accessor's host cost
-        base = self._mgr._view_cache(self) if (self._column and self._mgr is not None) else None
+        # (a view taken before an agent_capacity="auto" growth belongs to the
+        # manager's previous storage: no cached view of the current one)
+        base = self._mgr._view_cache(self) if (self._column and self._mgr is not None
+                                                and self._keep is self._mgr._hd) else None
         if base is not None:
             return base[:self.shape[0]]
         t = torch.as_tensor(self, device=dev)

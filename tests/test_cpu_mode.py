@@ -199,6 +199,38 @@ def test_auto_capacity_grows_without_drops():
     assert mgr.overflow() == orc.overflow() == 0
 
 
+def test_auto_capacity_old_views_keep_their_storage():
+    _old_views_keep_storage("cpu")
+
+
+@pytest.mark.gpu
+def test_auto_capacity_old_views_keep_their_storage_gpu():
+    _old_views_keep_storage("hip")
+
+
+def _old_views_keep_storage(exec_mode):
+    """A view (Tensor) taken before a growth still reads the storage it was
+    taken from, alive and unchanged, after the manager moved on (on the device
+    its to_torch() does not go through the new storage's view cache)."""
+    import madrona_bots as mb
+    mgr = mb.SimManager(0, 4, 69, 32, exec_mode=exec_mode, agent_capacity="auto")
+    old = mgr.position_tensor()
+    before = old.to_torch().clone()
+    mgr._grow_if_needed = lambda: None   # (only the forced growth below)
+    blob = mgr.save_checkpoint()
+    keep = mgr._hd
+    mgr._open(256)
+    import ctypes
+    mb._check(mb._lib.mbots_load_checkpoint(mgr._h, ctypes.c_void_p(blob.ctypes.data), blob.size))
+    del keep
+    assert mgr.agent_capacity == 256
+    assert torch.equal(old.to_torch(), before)
+    assert torch.equal(mgr.position_tensor().to_torch(), before)
+    mgr.step()
+    assert torch.equal(old.to_torch(), before)
+    assert old.to_torch().data_ptr() != mgr.position_tensor().to_torch().data_ptr()
+
+
 def test_checkpoint_across_capacities():
     """A checkpoint restores into a manager of another capacity when every
     world fits (the per-slot columns re-laid out); a world that does not fit
