@@ -1299,8 +1299,8 @@ constexpr float kInsideNear2 = 0.17f * 0.17f;  // disc centres this close are in
 template <int kCap>
 struct SensorLDS {
     // positions: food, then agents, then (kCap <= 128) 64 NaN sentinels that P1
-    // reads past nobj unchecked (the 256-slot class keeps its bounds checks: 2 KB
-    // more per block would cost it a block per CU)
+    // reads past nobj unchecked (the larger classes keep their bounds checks:
+    // 2 KB more per block would cost the 256-slot class a block per CU)
     float2 obj[kMaxFood + kCap + (kCap <= 128 ? 64 : 0)];
     float2 frot[kMaxFood];                    // food squares' (cos, sin)
     float2 hd[kCap];                          // agent headings
@@ -1625,7 +1625,7 @@ constexpr int kSensorWorlds = MB_SENSOR_WPB;   // worlds (waves) per sensor bloc
 #define MB_SENSOR_SPLIT_WAVES MB_SENSOR_WPB   // waves per block of the split sensor
 #endif
 // the launch bounds' minimum waves per SIMD: 8 (<= 64 VGPRs) for the 128-slot
-// class, 4 for the 256-slot one
+// class, 4 for the 256-slot one, 2 for the 512 / 1024 classes (LDS-bound there)
 __host__ __device__ constexpr int sensor_min_waves(int cap) { return cap <= 128 ? 8 : cap <= 256 ? 4 : 2; }
 // kDepth: fix_depth_alias (a depth byte per pixel besides the semantic one).
 // kSplit: kSplit waves share one world, each taking every kSplit-th key chunk
