@@ -18,10 +18,11 @@ ap.add_argument("--warmup", type=int, default=200)
 ap.add_argument("--stream-priority", type=int, default=None,
                 help="run on a new torch stream of this priority (lower = higher priority)")
 ap.add_argument("--no-kernel-timing", action="store_true")
+ap.add_argument("--capacity", type=int, default=128, help="agent_capacity (kernel class 128 / 256 / 512 / 1024)")
 a = ap.parse_args()
 if a.stream_priority is not None:
     torch.cuda.set_stream(torch.cuda.Stream(priority=a.stream_priority))
-m = mb.SimManager(0, a.worlds, 69, 32)
+m = mb.SimManager(0, a.worlds, 69, 32, agent_capacity=a.capacity)
 m.write_synthetic_actions(1234, 0)
 for t in range(a.warmup):
     m.step(); m.shift_observations(); m.write_synthetic_actions(1234, t + 1)
@@ -35,7 +36,7 @@ th = time.perf_counter() - t0   # the host's enqueue time (= dt when host-bound)
 torch.cuda.synchronize()
 dt = time.perf_counter() - t0
 kt = m.kernel_times()
-out = {"lib": os.path.basename(os.environ.get("MBOTS_LIB", "default")),
+out = {"lib": os.path.basename(os.environ.get("MBOTS_LIB", "default")), "capacity": a.capacity,
        "stream_priority": a.stream_priority,
        "agent_steps_per_s": (m.agent_steps() - s0) / dt, "ms_per_step": dt / a.steps * 1e3,
        "host_ms_per_step": th / a.steps * 1e3,
