@@ -1,6 +1,6 @@
-"""CPU, world_size 2 over gloo: world sharding is exact.
+"""CPU, world_size 2 and 8 over gloo: world sharding is exact.
 
-Each rank holds worlds [r*W/2, (r+1)*W/2) with world_offset = r*W/2 (the layout
+Each rank holds worlds [r*W/N, (r+1)*W/N) with world_offset = r*W/N (the layout
 bench.py uses on GPUs, no collective on the step), here through the product's
 CPU execution mode; every world's RNG key is split from its *global* index
 (sim.cpp:1238-1239), so the concatenated shard states must equal one oracle
@@ -60,15 +60,16 @@ def _run(sim):
         sim.shift_observations()
 
 
-def _worker(rank, port, q, reward_fixed, ghost):
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), MBOTS_CPU_THREADS="2")
+def _worker(rank, port, q, reward_fixed, ghost, ws):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                      MBOTS_CPU_THREADS="2" if ws <= 2 else "1")
     import madrona_bots as mb
-    dist.init_process_group("gloo", rank=rank, world_size=2)
-    half = W // 2
+    dist.init_process_group("gloo", rank=rank, world_size=ws)
+    per = W // ws
     # the last shard has no next shard: its last world reads past the table, as
-    # one device's last world does
-    sim = mb.SimManager(0, half, 69, 32, exec_mode="cpu", world_offset=rank * half,
-                        reward_fixed=reward_fixed, shard_ghost=ghost and rank == 0)
+    # one device's last world does (bench.py: shard_ghost=rank < world_size - 1)
+    sim = mb.SimManager(0, per, 69, 32, exec_mode="cpu", world_offset=rank * per,
+                        reward_fixed=reward_fixed, shard_ghost=ghost and rank < ws - 1)
     _run(sim)
     # bench.py's reductions: max time over ranks, sum of agent-steps
     t = torch.tensor([float(rank + 1)])
@@ -77,27 +78,31 @@ def _worker(rank, port, q, reward_fixed, ghost):
     dist.all_reduce(n, op=dist.ReduceOp.SUM)
     sc = sim.species_count_tensor().to_torch().numpy()
     rew = sim.reward_tensor(False).to_torch().numpy().ravel()
-    states = [None, None]
-    dist.all_gather_object(states, (_world_states(sim, rank * half, half, True),
-                                    _rewards_by_world(sc, rew, rank * half)))
+    states = [None] * ws
+    dist.all_gather_object(states, (_world_states(sim, rank * per, per, True),
+                                    _rewards_by_world(sc, rew, rank * per)))
     if rank == 0:
         q.put((float(t.item()), float(n.item()), states))
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("reward_fixed,ghost", [(True, False), (False, True), (False, False)])
-def test_two_shards_equal_one(reward_fixed, ghost):
+@pytest.mark.parametrize("reward_fixed,ghost,ws", [(True, False, 2), (False, True, 2), (False, False, 2),
+                                                   (False, True, 8)])
+def test_shards_equal_one(reward_fixed, ghost, ws):
+    """N shards (N = 2; and 8, the node the driver scales to: ranks of two
+    worlds each, every shard but the last with its ghost) equal one oracle
+    holding every world, and bench.py's max / sum reductions see every rank."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, port, q, reward_fixed, ghost)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, port, q, reward_fixed, ghost, ws)) for r in range(ws)]
     for p in procs:
         p.start()
-    tmax, nsum, states = q.get(timeout=120)
+    tmax, nsum, states = q.get(timeout=240)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    assert tmax == 2.0
+    assert tmax == float(ws)
     ref = po.OracleSim(W, 69, 32, reward_fixed=reward_fixed)
     _run(ref)
     assert nsum == ref.num_agents()
@@ -108,7 +113,7 @@ def test_two_shards_equal_one(reward_fixed, ghost):
             for k in st:
                 assert np.array_equal(st[k], full_states[w][k]), (w, k)
         for (w, s), r in shard_rew.items():
-            if not reward_fixed and not ghost and s == 3 and w == W // 2 - 1:
+            if not reward_fixed and not ghost and s == 3 and (w + 1) % (W // ws) == 0 and w != W - 1:
                 # no ghost: species 4 of the shard's last world reads past its
                 # table (0 here, world 8's rewards[0] unsharded)
                 assert r.shape == full_rew[(w, s)].shape
