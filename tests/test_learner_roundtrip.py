@@ -228,10 +228,9 @@ def _spawn(target, world, *args):
     return q.get(timeout=5)
 
 
-@pytest.mark.parametrize("slim", [False, True])
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world,slim", [(2, False), (2, True), (3, False), (3, True), (8, True)])
 def test_learner_roundtrip_gloo(world, slim):
-    """gather_learner / scatter_actions over gloo with 2 and 3 CPU-mode ranks:
+    """gather_learner / scatter_actions over gloo with 2, 3 and 8 CPU-mode ranks:
     rank 0's gathered tensors equal one manager of every world, step after
     step, while the learner's actions drive both (slim: provenance records
     and the learner's rebuild from the second step on)."""
