@@ -346,7 +346,8 @@ int mbots_kernel_times(mbots_handle *h, double ms[MBOTS_TK_COUNT],
                        uint64_t launches[MBOTS_TK_COUNT]);
 /* The step schedule the manager chose (diagnostics, no device call):
  * out[0] flags -- 1 K1-finder mode (the next K1 does not wait for the last
- * sensor), 2 fork by value, 4 join by value, 8 MBOTS_SWAP; out[1] the last
+ * sensor), 2 fork by value, 4 join by value, 8 MBOTS_SWAP, 16 mixed capacity
+ * classes (MBOTS_MIXED); out[1] the last
  * value-wait epoch raised; out[2] how often the epochs restarted from 0;
  * out[3] steps run.  CPU mode: all 0 but out[3]. */
 int mbots_schedule_info(mbots_handle *h, uint32_t out[4]);

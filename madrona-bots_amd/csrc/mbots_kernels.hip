@@ -219,7 +219,9 @@ constexpr int k1_min_blocks() { return kCap <= 128 ? 32 / kK1Worlds : kCap <= 25
 // kFinder: the finder slots this step reads computed here (world_finders)
 // instead of read from the last step's sensor, so K1 need not wait for it
 // (small world counts, where the step is a latency chain)
-template <int kCap, bool kFinder>
+// kSkipBig (mixed classes): worlds whose step could outgrow this class are
+// left to world_step_list_kernel
+template <int kCap, bool kFinder, bool kSkipBig = false>
 __global__ __launch_bounds__(64 * k1_worlds<kCap>(), k1_min_blocks<kCap>())
 __attribute__((amdgpu_num_sgpr(80))) void world_step_kernel(
     SimState S, ObsTable cur, int parity)
@@ -230,7 +232,10 @@ __attribute__((amdgpu_num_sgpr(80))) void world_step_kernel(
     const uint32_t wv = threadIdx.x >> 6;
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t w = uniform(blockIdx.x * kW1 + wv);
-    if (w < S.W) world_step<kCap, kFinder>(S, cur, lds[wv], fsc[kFinder ? wv : 0], w, lane);
+    // (mixed classes: a world whose step could outgrow the small class is the
+    // class kernel's, world_step_list_kernel)
+    const bool run = w < S.W && !(kSkipBig && k1_needs_class(uniform(S.n[w]), S.A));
+    if (run) world_step<kCap, kFinder>(S, cur, lds[wv], fsc[kFinder ? wv : 0], w, lane);
     // counter-major tile buckets: [counter][tile][bucket] (K2 reads one
     // counter's buckets as contiguous 16-B words)
     const size_t nent = (size_t)S.ntiles * kTileBuckets;
@@ -238,7 +243,7 @@ __attribute__((amdgpu_num_sgpr(80))) void world_step_kernel(
     if constexpr (kW1 == 1) {
         // one world per block: its species/agent counts go straight to the K2
         // scan tile (no block barrier: a block's LDS frees as its world ends)
-        if (w < S.Wx && lane < 5) {   // (a shard ghost, w >= Wx, is not counted)
+        if ((!kSkipBig || run) && w < S.Wx && lane < 5) {   // (a shard ghost, w >= Wx, is not counted)
             const int32_t *sc = lds[0].scount;
             atomicAdd(&tiles[lane * nent + (w / kTileWorlds) * kTileBuckets + blockIdx.x % kTileBuckets],
                       lane < 4 ? sc[lane] : sc[0] + sc[1] + sc[2] + sc[3]);
@@ -248,7 +253,8 @@ __attribute__((amdgpu_num_sgpr(80))) void world_step_kernel(
         // per-block species/agent counts -> the K2 scan tile (one atomic per counter)
         if (lane < 5) {   // (a shard ghost, w >= Wx, is not counted: its rows follow the table's)
             const int32_t *sc = lds[wv].scount;
-            blk[wv][lane] = (w < S.Wx) ? (lane < 4 ? sc[lane] : sc[0] + sc[1] + sc[2] + sc[3]) : 0;
+            blk[wv][lane] = ((!kSkipBig || run) && w < S.Wx) ? (lane < 4 ? sc[lane] : sc[0] + sc[1] + sc[2] + sc[3])
+                                                              : 0;
         }
         __syncthreads();
         if (threadIdx.x < 5) {
@@ -258,6 +264,34 @@ __attribute__((amdgpu_num_sgpr(80))) void world_step_kernel(
             const uint32_t tile = (blockIdx.x * kW1) / kTileWorlds;
             atomicAdd(&tiles[threadIdx.x * nent + tile * kTileBuckets + blockIdx.x % kTileBuckets], v);
         }
+    }
+}
+
+// K1 of the class kernel (mixed classes): the worlds the last K2 listed
+// (S.big_k1 of the other parity), a wave per world in a grid-stride loop,
+// each world's species / agent counts added to its scan tile itself
+template <int kCap>
+__global__ __launch_bounds__(64 * k1_worlds<kCap>(), k1_min_blocks<kCap>()) void world_step_list_kernel(
+    SimState S, ObsTable cur, int parity)
+{
+    constexpr int kW1 = k1_worlds<kCap>();
+    __shared__ WorldLDS<kCap> lds[kW1];
+    __shared__ FinderScratch<kCap> fsc[1];
+    const uint32_t wv = threadIdx.x >> 6;
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t lp = (uint32_t)parity ^ 1u;
+    const uint32_t cnt = uniform(S.big_cnt[lp * 2]);
+    const size_t nent = (size_t)S.ntiles * kTileBuckets;
+    int32_t *tiles = S.tiles + (size_t)parity * 5 * nent;
+    for (uint32_t i = blockIdx.x * kW1 + wv; i < cnt; i += gridDim.x * kW1) {
+        const uint32_t w = uniform((uint32_t)S.big_k1[(size_t)lp * S.W + i]);
+        world_step<kCap, false>(S, cur, lds[wv], fsc[0], w, lane);
+        if (w < S.Wx && lane < 5) {
+            const int32_t *sc = lds[wv].scount;
+            atomicAdd(&tiles[lane * nent + (w / kTileWorlds) * kTileBuckets + w % kTileBuckets],
+                      lane < 4 ? sc[lane] : sc[0] + sc[1] + sc[2] + sc[3]);
+        }
+        wave_sync();
     }
 }
 
@@ -864,6 +898,18 @@ __device__ __forceinline__ int wave_incl_scan(int v)
     return v;
 }
 
+// a wave's `take` lanes appended to list (one returning atomic per wave)
+__device__ __forceinline__ void list_append(bool take, int32_t *list, uint32_t *count, uint32_t w)
+{
+    const uint64_t m = ballot64(take);
+    if (m == 0ull) return;
+    const int lead = (int)__builtin_ctzll(m);
+    uint32_t base = 0;
+    if ((int)__lane_id() == lead) base = atomicAdd(count, (uint32_t)__popcll(m));
+    base = (uint32_t)__shfl((int)base, lead);
+    if (take) list[base + rank_below(m)] = (int32_t)w;
+}
+
 __global__ __launch_bounds__(1024) void scan_kernel(SimState S, int parity)
 {
     __shared__ int32_t s_pre[5], s_tot[5];
@@ -895,6 +941,13 @@ __global__ __launch_bounds__(1024) void scan_kernel(SimState S, int parity)
         const int4 sc = reinterpret_cast<const int4 *>(S.scount)[w];
         c[0] = sc.x; c[1] = sc.y; c[2] = sc.z; c[3] = sc.w;
         c[4] = sc.x + sc.y + sc.z + sc.w;
+    }
+    if (S.mixed) {   // the class lists of this parity (their counts cleared by the last K2)
+        const bool bk = w < S.W && k1_needs_class(c[4], S.A);
+        const bool bs = w < S.W && c[4] > kSmallCap;
+        list_append(bk, S.big_k1 + (size_t)parity * S.W, S.big_cnt + parity * 2, w);
+        list_append(bs, S.big_s + (size_t)parity * S.W, S.big_cnt + parity * 2 + 1, w);
+        if (b == 0 && t < 2) S.big_cnt[(parity ^ 1) * 2 + t] = 0u;   // the next K2's
     }
     int32_t inc[5];
 #pragma unroll
@@ -1023,6 +1076,15 @@ __global__ __launch_bounds__(1024) void tile_sum_kernel(SimState S, int parity)
         S.tiles[(size_t)parity * 5 * nent + e] = run;
         S.tiles[(size_t)(parity ^ 1) * 5 * nent + e] = 0;
     }
+}
+
+// mixed classes after a checkpoint load: the K1 class list of `slot` from S.n
+// (its count zeroed by the host beforehand)
+__global__ __launch_bounds__(256) void build_lists_kernel(SimState S, int slot)
+{
+    const uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool bk = w < S.W && k1_needs_class(S.n[w], S.A);
+    list_append(bk, S.big_k1 + (size_t)slot * S.W, S.big_cnt + slot * 2, w);
 }
 
 // ---------------------------------------------------------------------------
@@ -1633,35 +1695,19 @@ __host__ __device__ constexpr int sensor_min_waves(int cap) { return cap <= 128 
 // (<= 4096), where one wave per world leaves SIMDs idle and the step waits on
 // the latency of one world's serial chunk loop (4 waves per world: step -8 % at
 // 4096 worlds; 2 waves: -5 %; no gain at 8192).
-template <bool kDepth, int kSplit, int kCap, int kWaves>
-__global__ __launch_bounds__(64 * kWaves, sensor_min_waves(kCap)) void sensor_kernel(SimState S,
-                                                                                            ObsTable nxt)
+template <bool kDepth, int kSplit, int kCap, bool kSkipBig = false>
+__device__ __forceinline__ void sensor_world(const SimState &S, const ObsTable &nxt, SensorLDS<kCap> &L,
+                                             RayTab &R, uint32_t w, uint32_t wv, uint32_t lane)
 {
     constexpr int kG = kCap / 64;   // 64-slot groups
-    __shared__ SensorLDS<kCap> lds[kWaves];
-    __shared__ RayTab R;
-    const uint32_t wv = threadIdx.x >> 6;
-    const uint32_t lane = threadIdx.x & 63u;
-    static_assert(kWaves % kSplit == 0, "split must divide the block's waves");
-    constexpr uint32_t kWpb = kWaves / kSplit;   // worlds per block
-    uint32_t w = blockIdx.x * kWpb + wv / kSplit;
-    if (S.sorder) {
-        // blocks in dispatch order take every tile's heaviest worlds first,
-        // its lightest last (block b: tile b % ntiles, the tile's b / ntiles-th
-        // group of kWpb worlds; used when every tile is full), so the kernel's
-        // drain runs the cheapest worlds and a block's worlds cost about the same
-        const uint32_t b = blockIdx.x, tile = b % S.ntiles, q = b / S.ntiles;
-        w = (uint32_t)S.sorder[(size_t)tile * kTileWorlds + q * kWpb + wv / kSplit];
-    }
-    w = uniform(w);
     constexpr int kChunkStep = kKeyAgents * kSplit;
     const int kChunk0 = (int)(wv % kSplit) * kKeyAgents;
-    if (w >= S.W) return;
-    SensorLDS<kCap> &L = lds[wv];
     using K = typename SensorLDS<kCap>::key_t;
     constexpr bool depth = kDepth;
     SensorPrefetch pf;
     sensor_prefetch(S, w, lane, pf);
+    // (mixed classes: a world past the small class is the class kernel's)
+    if (kSkipBig && pf.n > kCap) return;
     // ray `lane`'s u and near point (the finder at 32: u = 0, {1.1, 0, 1.1}),
     // host-computed (upload_ray_table), loaded with the prefetch batch and
     // stored to the block's table after the staging below
@@ -2051,6 +2097,44 @@ __global__ __launch_bounds__(64 * kWaves, sensor_min_waves(kCap)) void sensor_ke
 #else
     (void)mbc;
 #endif
+    }
+}
+
+// kList (mixed classes): the worlds K2 listed as past the small class
+// (S.big_s of this step's parity), a wave per world in a grid-stride loop;
+// kSkipBig: the small class's launch beside it, which leaves those worlds
+template <bool kDepth, int kSplit, int kCap, int kWaves, bool kList = false, bool kSkipBig = false>
+__global__ __launch_bounds__(64 * kWaves, sensor_min_waves(kCap)) void sensor_kernel(SimState S,
+                                                                                            ObsTable nxt)
+{
+    __shared__ SensorLDS<kCap> lds[kWaves];
+    __shared__ RayTab R;
+    const uint32_t wv = threadIdx.x >> 6;
+    const uint32_t lane = threadIdx.x & 63u;
+    static_assert(kWaves % kSplit == 0, "split must divide the block's waves");
+    if constexpr (kList) {
+        static_assert(kSplit == 1, "the class kernel renders a world per wave");
+        const uint32_t par = S.list_par;
+        const uint32_t cnt = uniform(S.big_cnt[par * 2 + 1]);
+        for (uint32_t i = blockIdx.x * kWaves + wv; i < cnt; i += gridDim.x * kWaves) {
+            const uint32_t w = uniform((uint32_t)S.big_s[(size_t)par * S.W + i]);
+            sensor_world<kDepth, 1, kCap>(S, nxt, lds[wv], R, w, wv, lane);
+            wave_sync();
+        }
+    } else {
+        constexpr uint32_t kWpb = kWaves / kSplit;   // worlds per block
+        uint32_t w = blockIdx.x * kWpb + wv / kSplit;
+        if (S.sorder) {
+            // blocks in dispatch order take every tile's heaviest worlds first,
+            // its lightest last (block b: tile b % ntiles, the tile's b / ntiles-th
+            // group of kWpb worlds; used when every tile is full), so the kernel's
+            // drain runs the cheapest worlds and a block's worlds cost about the same
+            const uint32_t b = blockIdx.x, tile = b % S.ntiles, q = b / S.ntiles;
+            w = (uint32_t)S.sorder[(size_t)tile * kTileWorlds + q * kWpb + wv / kSplit];
+        }
+        w = uniform(w);
+        if (w >= S.W) return;
+        sensor_world<kDepth, kSplit, kCap, kSkipBig>(S, nxt, lds[wv], R, w, wv, lane);
     }
 }
 
@@ -2655,9 +2739,25 @@ hipError_t launch_world_step(const SimState &S, const ObsTable &cur, int parity,
         else hipExtLaunchKernelGGL(kern, grid, blk, 0u, st, nullptr, done, 0u, S, cur, parity);   // on the packet
     };
     // (K1-finder mode is a <= 256-slot mode: its camera slots are bytes)
-    if (S.cap <= 128)
-        S.k1_finder ? go(world_step_kernel<128, true>, kK1Worlds) : go(world_step_kernel<128, false>, kK1Worlds);
-    else if (S.cap <= 256)
+    if (S.cap <= 128 || S.mixed) {
+        // mixed classes: the small kernel for every world that fits it, then the
+        // class kernel over the worlds the last K2 listed (a fixed grid; `done`
+        // rides on the last dispatch)
+        if (!S.mixed)
+            S.k1_finder ? go(world_step_kernel<128, true>, kK1Worlds) : go(world_step_kernel<128, false>, kK1Worlds);
+        else {
+            hipLaunchKernelGGL((world_step_kernel<128, false, true>), dim3((S.W + kK1Worlds - 1) / kK1Worlds),
+                               dim3(64 * kK1Worlds), 0, st, S, cur, parity);
+            auto list = [&](auto kern, int wpb) {
+                const dim3 grid(std::max(1u, std::min((S.W + wpb - 1) / wpb, 1024u))), blk(64 * wpb);
+                if (!done) hipLaunchKernelGGL(kern, grid, blk, 0, st, S, cur, parity);
+                else hipExtLaunchKernelGGL(kern, grid, blk, 0u, st, nullptr, done, 0u, S, cur, parity);
+            };
+            if (S.cap <= 256) list(world_step_list_kernel<256>, k1_worlds<256>());
+            else if (S.cap <= 512) list(world_step_list_kernel<512>, k1_worlds<512>());
+            else list(world_step_list_kernel<1024>, k1_worlds<1024>());
+        }
+    } else if (S.cap <= 256)
         S.k1_finder ? go(world_step_kernel<256, true>, kK1Worlds) : go(world_step_kernel<256, false>, kK1Worlds);
     else if (S.cap <= 512)
         go(world_step_kernel<512, false>, k1_worlds<512>());
@@ -2678,6 +2778,11 @@ hipError_t launch_scan(const SimState &S, int parity, hipStream_t st, hipEvent_t
         return hipEventRecord(done, st);
     }
     hipExtLaunchKernelGGL(scan_kernel, dim3(S.ntiles), dim3(1024), 0, st, nullptr, done, 0u, S, parity);
+    return hipGetLastError();
+}
+hipError_t launch_build_lists(const SimState &S, int slot, hipStream_t st)
+{
+    hipLaunchKernelGGL(build_lists_kernel, dim3((S.W + 255) / 256), dim3(256), 0, st, S, slot);
     return hipGetLastError();
 }
 hipError_t launch_export_rows(const SimState &S, const ObsTable &nxt, int init, hipStream_t st)
@@ -2770,7 +2875,7 @@ hipError_t launch_move(const SimState &S, const ObsTable &cur, const ObsTable &n
         }                                                                                   \
     } while (0)
 
-template <int kCap>
+template <int kCap, bool kSkipBig = false>
 static void launch_sensor_cap(const SimState &S, const ObsTable &nxt, hipStream_t st, hipEvent_t done,
                               bool plain_events)
 {
@@ -2786,20 +2891,39 @@ static void launch_sensor_cap(const SimState &S, const ObsTable &nxt, hipStream_
         constexpr int kWv = MB_SENSOR_SPLIT_WAVES, kWpb = kWv / MB_SENSOR_SPLIT;
         const dim3 grid((S.W + kWpb - 1) / kWpb), blk(64 * kWv);
         if (fixd)
-            MB_LAUNCH_EV((sensor_kernel<true, MB_SENSOR_SPLIT, kCap, kWv>), grid, blk, st, done, plain_events, S, nxt);
+            MB_LAUNCH_EV((sensor_kernel<true, MB_SENSOR_SPLIT, kCap, kWv, false, kSkipBig>), grid, blk, st, done, plain_events, S, nxt);
         else
-            MB_LAUNCH_EV((sensor_kernel<false, MB_SENSOR_SPLIT, kCap, kWv>), grid, blk, st, done, plain_events, S, nxt);
+            MB_LAUNCH_EV((sensor_kernel<false, MB_SENSOR_SPLIT, kCap, kWv, false, kSkipBig>), grid, blk, st, done, plain_events, S, nxt);
     } else {
         const dim3 grid((S.W + kSensorWorlds - 1) / kSensorWorlds), blk(64 * kSensorWorlds);
         if (fixd)
-            MB_LAUNCH_EV((sensor_kernel<true, 1, kCap, kSensorWorlds>), grid, blk, st, done, plain_events, S, nxt);
+            MB_LAUNCH_EV((sensor_kernel<true, 1, kCap, kSensorWorlds, false, kSkipBig>), grid, blk, st, done, plain_events, S, nxt);
         else
-            MB_LAUNCH_EV((sensor_kernel<false, 1, kCap, kSensorWorlds>), grid, blk, st, done, plain_events, S, nxt);
+            MB_LAUNCH_EV((sensor_kernel<false, 1, kCap, kSensorWorlds, false, kSkipBig>), grid, blk, st, done, plain_events, S, nxt);
     }
+}
+// mixed classes: the class kernel over the worlds this step's K2 listed (a
+// fixed grid of one-wave blocks looping over the list)
+template <int kCap>
+static void launch_sensor_list(const SimState &S, const ObsTable &nxt, hipStream_t st, hipEvent_t done,
+                               bool plain_events)
+{
+    const dim3 grid(std::max(1u, std::min(S.W, 2048u))), blk(64);
+    if (S.flags & kFlagFixDepth)
+        MB_LAUNCH_EV((sensor_kernel<true, 1, kCap, 1, true>), grid, blk, st, done, plain_events, S, nxt);
+    else
+        MB_LAUNCH_EV((sensor_kernel<false, 1, kCap, 1, true>), grid, blk, st, done, plain_events, S, nxt);
 }
 hipError_t launch_sensor(const SimState &S, const ObsTable &nxt, hipStream_t st, hipEvent_t done,
                          bool plain_events)
 {
+    if (S.mixed) {
+        launch_sensor_cap<128, true>(S, nxt, st, nullptr, plain_events);
+        if (S.cap <= 256) launch_sensor_list<256>(S, nxt, st, done, plain_events);
+        else if (S.cap <= 512) launch_sensor_list<512>(S, nxt, st, done, plain_events);
+        else launch_sensor_list<1024>(S, nxt, st, done, plain_events);
+        return hipGetLastError();
+    }
     if (S.cap <= 128) launch_sensor_cap<128>(S, nxt, st, done, plain_events);
     else if (S.cap <= 256) launch_sensor_cap<256>(S, nxt, st, done, plain_events);
     else if (S.cap <= 512) launch_sensor_cap<512>(S, nxt, st, done, plain_events);

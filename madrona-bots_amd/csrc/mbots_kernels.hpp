@@ -70,7 +70,21 @@ struct SimState {
     const uint8_t *pdepth_src;
     uint32_t Wx;                    // exported worlds: W, or W - 1 with the shard ghost (the
                                     // last world, its rows placed after every exported row)
+    // mixed capacity classes (agent_capacity > 128 outside K1-finder mode): the
+    // 128-slot kernels take every world that fits them and the class kernels
+    // only the worlds K2 listed -- big_k1: 2 n + A > 128 (the next K1 could
+    // overflow 128 slots), big_s: n > 128 (this step's sensor) -- each [2][W]
+    // by step parity, with their counts in big_cnt[parity][2]
+    uint32_t mixed;
+    uint32_t list_par;              // the parity whose lists this launch reads (host-set)
+    int32_t *big_k1, *big_s;
+    uint32_t *big_cnt;
 };
+
+// the small kernel class of mixed-class dispatch
+constexpr int kSmallCap = 128;
+// a world whose next K1 needs the class kernel: it may end with 2 n + A agents
+__host__ __device__ inline bool k1_needs_class(int n, uint32_t A) { return 2 * n + (int)A > kSmallCap; }
 
 inline void swap_state(SimState &S)
 {
@@ -109,6 +123,9 @@ hipError_t launch_world_step(const SimState &S, const ObsTable &cur, int parity,
 // plain_events: record `done` with hipEventRecord (stream capture) instead of on the dispatch
 hipError_t launch_scan(const SimState &S, int parity, hipStream_t st, hipEvent_t done = nullptr,
                        bool plain_events = false);
+// mixed classes: the K1 class list of slot `slot` rebuilt from S.n (after a
+// checkpoint load; K2 builds it every step)
+hipError_t launch_build_lists(const SimState &S, int slot, hipStream_t st);
 hipError_t launch_export_rows(const SimState &S, const ObsTable &nxt, int init, hipStream_t st);
 // K4 parts (DESIGN.md "Deferred Prev moves"): Action + HiddenState; the same
 // also into PrevAction / PrevHiddenState (the fused shift); the prev sensor;

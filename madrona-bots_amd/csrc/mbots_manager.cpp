@@ -309,6 +309,9 @@ size_t layout(mbots_handle *h, Arena &a)
     S.tiles = a.take<int32_t>((size_t)2 * S.ntiles * kTileBuckets * 5);
     S.agent_steps = a.take<unsigned long long>(1);
     S.raytab = a.take<float4>(36);
+    S.big_k1 = a.take<int32_t>(2 * W);   // mixed capacity classes (K2's lists)
+    S.big_s = a.take<int32_t>(2 * W);
+    S.big_cnt = a.take<uint32_t>(4);
     h->sorder2[0] = h->sorder2[1] = nullptr;
     if (sensor_order_used((uint32_t)W)) {
         h->sorder2[0] = a.take<int32_t>(W);
@@ -824,6 +827,15 @@ int mbots_create(const mbots_config *cfg_in, mbots_handle **out)
     // (the K1 finder pass keeps camera slots in bytes: a <= 256-slot mode)
     h->k1_finder = S.W <= MB_K1_FINDER_MAX && S.cap <= 256;
     S.k1_finder = h->k1_finder ? 1u : 0u;
+    {
+        // mixed capacity classes (round 6): above 128 slots the 128-slot K1
+        // and sensor take every world that fits them and the class kernels
+        // only the worlds K2 lists (DESIGN.md "Capacity"); MBOTS_MIXED=0 runs
+        // every world in the class kernels
+        const char *e = std::getenv("MBOTS_MIXED");
+        const bool want = !(e && *e == '0');
+        S.mixed = (want && S.cap > (uint32_t)mbots::kSmallCap && !h->k1_finder) ? 1u : 0u;
+    }
 
     int rc = MBOTS_OK;
     auto check = [&](hipError_t e, const char *what) {
@@ -1098,6 +1110,7 @@ int mbots_step(mbots_handle *h, void *stream)
         h->S.psem_src = h->T[h->tb].sem;
         h->S.pdepth_src = (h->cfg.flags & MBOTS_FLAG_FIX_DEPTH_ALIAS) ? h->T[h->tb].depth : nullptr;
     }
+    h->S.list_par = (uint32_t)par;   // (mixed classes: this step's K2 lists)
     rc = timed(h, MBOTS_TK_SENSOR, h->aux, [&] {
         return mbots::launch_sensor(h->S, nxt, h->aux, h->ev_join[jcur], capturing);
     });
@@ -1836,6 +1849,11 @@ int mbots_load_checkpoint(mbots_handle *h, const void *src, uint64_t bytes)
         p += segs_src[i].bytes;
     }
     HIP_TRY(hipMemset(h->S.tiles, 0, (size_t)2 * h->S.ntiles * mbots::kTileBuckets * 5 * sizeof(int32_t)));
+    if (h->S.mixed) {
+        // the first K1 after the load (parity 0) reads the class list of slot 1
+        HIP_TRY(hipMemset(h->S.big_cnt, 0, 4 * sizeof(uint32_t)));
+        HIP_TRY(mbots::launch_build_lists(h->S, 1, nullptr));
+    }
     h->tb = 0;
     h->parity = 0;
     h->last_join = -1;
@@ -1916,7 +1934,8 @@ int mbots_schedule_info(mbots_handle *h, uint32_t out[4])
         out[3] = (uint32_t)h->steps;
         return MBOTS_OK;
     }
-    out[0] = (h->k1_finder ? 1u : 0u) | (h->sig_fork ? 2u : 0u) | (h->sig_join ? 4u : 0u) | (h->swap ? 8u : 0u);
+    out[0] = (h->k1_finder ? 1u : 0u) | (h->sig_fork ? 2u : 0u) | (h->sig_join ? 4u : 0u) | (h->swap ? 8u : 0u) |
+             (h->S.mixed ? 16u : 0u);
     out[1] = h->epoch;
     out[2] = h->epoch_wraps;
     out[3] = (uint32_t)h->steps;

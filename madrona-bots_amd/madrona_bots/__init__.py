@@ -766,13 +766,14 @@ class SimManager:
 
     def schedule_info(self):
         """The step schedule in use (mbots_schedule_info): {"k1_finder",
-        "fork_by_value", "join_by_value", "swap": bool, "epoch", "epoch_wraps",
-        "steps": int}."""
+        "fork_by_value", "join_by_value", "swap", "mixed_classes": bool,
+        "epoch", "epoch_wraps", "steps": int}."""
         v = (ctypes.c_uint32 * 4)()
         _check(_lib.mbots_schedule_info(self._h, v))
         f = v[0]
         return {"k1_finder": bool(f & 1), "fork_by_value": bool(f & 2), "join_by_value": bool(f & 4),
-                "swap": bool(f & 8), "epoch": int(v[1]), "epoch_wraps": int(v[2]), "steps": int(v[3])}
+                "swap": bool(f & 8), "mixed_classes": bool(f & 16), "epoch": int(v[1]),
+                "epoch_wraps": int(v[2]), "steps": int(v[3])}
 
     def kernel_times(self):
         """{kernel: (total_ms, launches)} since enable_kernel_timing()."""

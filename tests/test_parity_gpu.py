@@ -531,6 +531,44 @@ def test_checkpoint_across_capacities_gpu():
         mb.SimManager(0, 4100, 69, 32, agent_capacity=32).load_checkpoint(blob.tobytes())
 
 
+@pytest.mark.parametrize("cap,W,steps", [(512, 4100, 24), (256, 16400, 16), (1024, 3000, 20)])
+def test_mixed_classes_equal_single_class(cap, W, steps, monkeypatch):
+    """Mixed capacity classes (the 128-slot K1 and sensor for every world that
+    fits them, the class kernels for the worlds K2 lists) against the same
+    manager running every world in the class kernels (MBOTS_MIXED=0), under the
+    breed-heavy stream that makes some worlds outgrow 128 slots while others do
+    not: every column bitwise equal after every step and shift (the
+    single-class path is the oracle-checked one above); 16400 worlds take the
+    swapped schedule and K2's population order, 4100 the split sensor."""
+    import madrona_bots as mb
+    monkeypatch.setenv("MBOTS_MIXED", "0")
+    ref = mb.SimManager(0, W, 69, 32, agent_capacity=cap)
+    monkeypatch.delenv("MBOTS_MIXED")
+    mgr = mb.SimManager(0, W, 69, 32, agent_capacity=cap)
+    assert mgr.schedule_info()["mixed_classes"] and not ref.schedule_info()["mixed_classes"]
+    from simpair import COLUMNS, bits, gpu_column
+    big = 0
+    for t in range(steps):
+        a = _breed_heavy(mgr.num_agents(), t).to("cuda")
+        for m in (mgr, ref):
+            m.action_tensor(False).to_torch().copy_(a)
+            m.step()
+        n = mgr.species_count_tensor().to_torch().sum(1)
+        k = int((2 * n + 32 > 128).sum())   # worlds the next K1 runs in the class kernel
+        big = max(big, k if k < W else 0)
+        for where in ("step", "shift"):
+            assert mgr.num_agents() == ref.num_agents(), (t, where)
+            for name, _ in COLUMNS + [("depth_tensor", None)]:
+                for prev in (False, True):
+                    g, r = gpu_column(mgr, name, prev), gpu_column(ref, name, prev)
+                    assert np.array_equal(bits(g), bits(r)), (t, where, name, prev)
+            if where == "step":
+                for m in (mgr, ref):
+                    m.shift_observations()
+    assert mgr.overflow() == ref.overflow()
+    assert big > 0   # both kinds of world were on the device at once
+
+
 @pytest.mark.parametrize("cap,W", [(512, 4100), (1024, 8192)])
 def test_large_capacity_classes_bench_stream(cap, W):
     """The 512 / 1024-slot classes at world counts past the split sensor and
