@@ -374,6 +374,12 @@ const char *mbots_last_error(void);
  *   rows (the sensor's chain sets the step's pace: -2 % against the forked
  *   schedule); MBOTS_SWAP=0 keeps K1 and K2 on the caller's stream and forks
  *   the sensor off after K2.
+ * MBOTS_MIXED (read at mbots_create; agent_capacity above 128, outside the
+ *   K1 finder mode): by default ("1") the 128-slot K1 and sensor run every
+ *   world that fits them and the capacity class's kernels only the worlds K2
+ *   lists (a world whose step could outgrow 128 slots, one with more than 128
+ *   agents); MBOTS_MIXED=0 runs every world in the class's kernels (the same
+ *   bits, slower).
  * MBOTS_CPU_THREADS: host threads of MBOTS_EXEC_CPU (default: the machine's
  *   hardware threads, at most 16).
  * MBOTS_EPOCH_START=<n> (read at mbots_create; a test hook): the value waits
