@@ -590,15 +590,17 @@ def test_large_capacity_classes_bench_stream(cap, W):
         assert not errs, errs[:5]
 
 
-@pytest.mark.parametrize("W", [64, 1024, 4100])
-def test_graph_capture_replays_match_oracle(W):
+@pytest.mark.parametrize("W,cap", [(64, 128), (1024, 128), (4100, 128), (4100, 512)])
+def test_graph_capture_replays_match_oracle(W, cap):
     """Steps recorded into a HIP graph (torch.cuda.graph; the fork / join
     events become capturable records, mbots_join ends the capture) and replayed
     equal the same call sequence run eagerly on the oracle, bitwise.  A replay
-    repeats the captured action-stream step numbers; the oracle mirrors that."""
+    repeats the captured action-stream step numbers; the oracle mirrors that.
+    (cap 512: the mixed capacity classes' K2 lists and class kernels inside
+    the graph.)"""
     import madrona_bots as mb
-    mgr = mb.SimManager(0, W, 69, 32)
-    orc = pyoracle.OracleSim(W, 69, 32, num_threads=8)
+    mgr = mb.SimManager(0, W, 69, 32, agent_capacity=cap)
+    orc = pyoracle.OracleSim(W, 69, 32, cap=cap, num_threads=8)
     s = torch.cuda.Stream()
     s.wait_stream(torch.cuda.current_stream())
     g = torch.cuda.CUDAGraph()
