@@ -288,6 +288,11 @@ int mbots_write_actions(mbots_handle *h, const int32_t *action, const float *hid
                         void *stream);
 /* every table row: N plus the shard ghost's (which follow row N) */
 int mbots_num_rows(mbots_handle *h, uint32_t *out);
+/* the largest world population after the last step (the shard ghost
+ * included): waits for that step's row counts only (K2), not for its sensor
+ * or the caller's chain -- what SimManager(agent_capacity="auto") checks
+ * before each step (a step adds at most n births and A respawns) */
+int mbots_max_population(mbots_handle *h, uint32_t *out);
 
 /* Checkpoint / restore (the reference has none): the live state
  * after the last step (agent SoA, RNG keys/counters, food, the current export

@@ -41,6 +41,12 @@ public:
     uint32_t num_agents() const { return N_; }
     // every table row: N plus the shard ghost's (which follow row N)
     uint32_t num_rows() const { return N_ + (W_ > Wx_ ? (uint32_t)n_[Wx_] : 0u); }
+    uint32_t max_population() const
+    {
+        int32_t m = 0;
+        for (int32_t v : n_) m = v > m ? v : m;
+        return (uint32_t)m;
+    }
     uint32_t world_offset_of(uint32_t w) const { return (uint32_t)world_off_[w]; }
     uint64_t agent_steps() const { return agent_steps_; }
     uint64_t overflow() const;

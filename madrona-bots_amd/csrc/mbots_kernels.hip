@@ -915,6 +915,7 @@ __global__ __launch_bounds__(1024) void scan_kernel(SimState S, int parity)
     __shared__ int32_t s_pre[5], s_tot[5];
     __shared__ int32_t s_wave[16][5];
     __shared__ int32_t s_hist[256];
+    __shared__ int32_t s_max[16];
     const int t = threadIdx.x, b = blockIdx.x;
     const int wv = t >> 6, lane = t & 63;
     const uint32_t nent = S.ntiles * kTileBuckets;   // a multiple of 8: 16-B words
@@ -952,6 +953,11 @@ __global__ __launch_bounds__(1024) void scan_kernel(SimState S, int parity)
     int32_t inc[5];
 #pragma unroll
     for (int k = 0; k < 5; ++k) inc[k] = wave_incl_scan(c[k]);
+    {   // the tile's largest world (kTotMaxPop: agent_capacity="auto" reads it)
+        int32_t mx = c[4];
+        for (int o = 32; o > 0; o >>= 1) mx = max(mx, __shfl_xor(mx, o));
+        if (lane == 0) s_max[wv] = mx;
+    }
     if (lane == 63) {
 #pragma unroll
         for (int k = 0; k < 5; ++k) s_wave[wv][k] = inc[k];
@@ -969,6 +975,12 @@ __global__ __launch_bounds__(1024) void scan_kernel(SimState S, int parity)
         }
     }
     __syncthreads();
+    if (t == 32 && S.totals_host) {   // this tile's largest world into the pinned mirror
+        int32_t mx = 0;
+        for (int i = 0; i < 16; ++i) mx = max(mx, s_max[i]);
+        __hip_atomic_store(S.totals_host + kTotMaxPop + b, (uint32_t)mx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __threadfence_system();
+    }
     if (t < 5) {
         int32_t run = 0;
         for (int i = 0; i < 16; ++i) { const int32_t v = s_wave[i][t]; s_wave[i][t] = run; run += v; }

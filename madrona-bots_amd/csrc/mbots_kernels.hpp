@@ -104,6 +104,8 @@ struct ObsTable {
 };
 
 constexpr int kTotRows = 5;   // totals[kTotRows]: rows the moves / shift / checkpoints cover
+constexpr int kTotMaxPop = 8;     // totals_host[kTotMaxPop + tile]: the tile's largest world
+                                  // population after the last K2 (the pinned mirror only)
 constexpr int kTotOverflow = 6;   // totals[kTotOverflow]: births / respawns dropped at the
                                   // capacity cap so far (exported worlds; K1 adds, K2 mirrors)
 uint32_t scan_tiles(uint32_t W);

@@ -138,6 +138,7 @@ struct mbots_handle {
     uint32_t join_epoch = 0;          // the epoch raised after the last sensor (0: none;
                                       // the join is then the sensor's event)
     bool totals_ok = false;           // h_totals holds the last step's counts (synchronised)
+    bool maxpop_stale = false;        // no K2 since a checkpoint load: the tile maxima are old
     int forced = 0;                   // deferred parts the caller's reads needed since the
                                       // last step (kMove*): the next step prefetches them
     int prefetched = 0;               // parts this step prefetched and no shift superseded
@@ -842,7 +843,9 @@ int mbots_create(const mbots_config *cfg_in, mbots_handle **out)
         if (e != hipSuccess && rc == MBOTS_OK)
             rc = fail(MBOTS_E_HIP, std::string(what) + ": " + hipGetErrorString(e));
     };
-    check(hipHostMalloc((void **)&h->h_totals, 8 * sizeof(uint32_t), hipHostMallocMapped),
+    // (8 totals, then each scan tile's largest world: mbots_max_population)
+    check(hipHostMalloc((void **)&h->h_totals, ((size_t)mbots::kTotMaxPop + S.ntiles) * sizeof(uint32_t),
+                        hipHostMallocMapped),
           "hipHostMalloc");
     if (rc == MBOTS_OK)
         check(hipHostGetDevicePointer((void **)&S.totals_host, h->h_totals, 0),
@@ -1088,6 +1091,7 @@ int mbots_step(mbots_handle *h, void *stream)
     // cleared here, after every materialisation above that may sync the last ones)
     h->totals_ok = false;
     rc = timed(h, MBOTS_TK_SCAN, kst, [&] { return mbots::launch_scan(h->S, par, kst, h->ev_totals, capturing); });
+    h->maxpop_stale = false;
     h->S.epoch = 0;
     if (rc) return rc;
     // fork after K2: the K3b sensor (VALU-bound; it derives the export rows from
@@ -1595,6 +1599,34 @@ int mbots_unpack_learner(const void *records, uint64_t rows, int32_t with_depth,
     return MBOTS_OK;
 }
 
+int mbots_max_population(mbots_handle *h, uint32_t *out)
+{
+    if (!h || !out) return fail(MBOTS_E_INVALID, "null argument");
+    if (h->cpu) {
+        *out = h->cpu->max_population();
+        return MBOTS_OK;
+    }
+    HIP_TRY(hipSetDevice(h->device));
+    if (h->maxpop_stale) {   // (after a checkpoint load, until the next step's K2)
+        HIP_TRY(hipDeviceSynchronize());
+        std::vector<int32_t> n(h->S.W);
+        HIP_TRY(hipMemcpy(n.data(), h->S.n, n.size() * sizeof(int32_t), hipMemcpyDeviceToHost));
+        int32_t mx = 0;
+        for (int32_t v : n) mx = std::max(mx, v);
+        *out = (uint32_t)mx;
+        return MBOTS_OK;
+    }
+    // the last step's K2 published each tile's largest world with the row
+    // counts: waiting for it waits for K2 only, not for the step's sensor or
+    // the caller's chain
+    if (int rc = sync_totals(h)) return rc;
+    uint32_t mx = 0;
+    for (uint32_t t = 0; t < h->S.ntiles; ++t)
+        mx = std::max(mx, __atomic_load_n(&h->h_totals[mbots::kTotMaxPop + t], __ATOMIC_RELAXED));
+    *out = mx;
+    return MBOTS_OK;
+}
+
 int mbots_num_rows(mbots_handle *h, uint32_t *out)
 {
     if (!h || !out) return fail(MBOTS_E_INVALID, "null argument");
@@ -1877,6 +1909,7 @@ int mbots_load_checkpoint(mbots_handle *h, const void *src, uint64_t bytes)
     if (rc) return rc;
     HIP_TRY(hipDeviceSynchronize());
     h->ovf_reported = h->h_totals[mbots::kTotOverflow];   // drops before the checkpoint were reported then
+    h->maxpop_stale = true;
     return MBOTS_OK;
 }
 

@@ -95,6 +95,7 @@ def _load():
         "mbots_enable_kernel_timing": [vp, i32],
         "mbots_kernel_times": [vp, P(ctypes.c_double), P(ctypes.c_uint64)],
         "mbots_schedule_info": [vp, P(u32)],
+        "mbots_max_population": [vp, P(u32)],
     }
     for name, args in sig.items():
         fn = getattr(L, name)
@@ -391,7 +392,8 @@ class SimManager:
 
     agent_capacity="auto" grows the worlds' capacity instead of dropping
     agents: before each step() the manager reads the largest world population
-    n (one synchronisation) and, when the step could overflow -- a step adds at
+    n (mbots_max_population: a wait for the last step's row counts, not for
+    its sensor) and, when the step could overflow -- a step adds at
     most n births (one per agent, sim.cpp:561-564) and A respawns
     (:830-834) -- moves its state into the next capacity class (128, 256, 512,
     1024) through a checkpoint, so the run stays the reference's (bitwise equal
@@ -443,9 +445,11 @@ class SimManager:
         could overflow this one (at most 2 n + A agents after it)."""
         if self.agent_capacity >= MAX_CAPACITY:
             return
-        sc = self.species_count_tensor().to_torch()
-        n = int(sc.sum(dim=1).max()) if sc.numel() else 0
-        need = 2 * n + self._cfg[3]
+        # (waits for the last step's row counts only, not for its sensor or the
+        # caller's chain: the device stays fed while the host runs one step ahead)
+        v = ctypes.c_uint32()
+        _check(_lib.mbots_max_population(self._h, ctypes.byref(v)))
+        need = 2 * int(v.value) + self._cfg[3]
         if need <= self.agent_capacity:
             return
         blob = self.save_checkpoint()

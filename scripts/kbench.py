@@ -18,11 +18,11 @@ ap.add_argument("--warmup", type=int, default=200)
 ap.add_argument("--stream-priority", type=int, default=None,
                 help="run on a new torch stream of this priority (lower = higher priority)")
 ap.add_argument("--no-kernel-timing", action="store_true")
-ap.add_argument("--capacity", type=int, default=128, help="agent_capacity (kernel class 128 / 256 / 512 / 1024)")
+ap.add_argument("--capacity", default="128", help='agent_capacity (kernel class 128 / 256 / 512 / 1024, or "auto")')
 a = ap.parse_args()
 if a.stream_priority is not None:
     torch.cuda.set_stream(torch.cuda.Stream(priority=a.stream_priority))
-m = mb.SimManager(0, a.worlds, 69, 32, agent_capacity=a.capacity)
+m = mb.SimManager(0, a.worlds, 69, 32, agent_capacity=a.capacity if a.capacity == "auto" else int(a.capacity))
 m.write_synthetic_actions(1234, 0)
 for t in range(a.warmup):
     m.step(); m.shift_observations(); m.write_synthetic_actions(1234, t + 1)

@@ -502,6 +502,33 @@ def test_auto_capacity_grows_without_drops(W, steps):
     assert mgr.overflow() == orc.overflow() == 0
 
 
+def test_max_population_matches_species_counts():
+    """mbots_max_population (K2's per-tile maxima in the pinned mirror; after a
+    checkpoint load, until the next K2, read from the device) equals the
+    largest world of species_count after every step, on the plain and the
+    swapped schedule."""
+    import ctypes
+    import madrona_bots as mb
+
+    def maxpop(m):
+        v = ctypes.c_uint32()
+        mb._check(mb._lib.mbots_max_population(m._h, ctypes.byref(v)))
+        return int(v.value)
+
+    for W in (3000, 16400):
+        m = mb.SimManager(0, W, 69, 32)
+        for t in range(12):
+            a = _breed_heavy(m.num_agents(), t).to("cuda")
+            m.action_tensor(False).to_torch().copy_(a)
+            m.step()
+            assert maxpop(m) == int(m.species_count_tensor().to_torch().sum(1).max()), (W, t)
+            m.shift_observations()
+        blob = m.save_checkpoint()
+        b = mb.SimManager(0, W, 69, 32)
+        b.load_checkpoint(blob)
+        assert maxpop(b) == maxpop(m)
+
+
 def test_checkpoint_across_capacities_gpu():
     """A device checkpoint restores into managers of other capacity classes
     (per-slot columns re-laid out world by world) and the runs continue
