@@ -953,7 +953,7 @@ __global__ __launch_bounds__(1024) void scan_kernel(SimState S, int parity)
     int32_t inc[5];
 #pragma unroll
     for (int k = 0; k < 5; ++k) inc[k] = wave_incl_scan(c[k]);
-    {   // the tile's largest world (kTotMaxPop: agent_capacity="auto" reads it)
+    if (S.track_maxpop) {   // the tile's largest world (kTotMaxPop: mbots_max_population)
         int32_t mx = c[4];
         for (int o = 32; o > 0; o >>= 1) mx = max(mx, __shfl_xor(mx, o));
         if (lane == 0) s_max[wv] = mx;
@@ -975,7 +975,7 @@ __global__ __launch_bounds__(1024) void scan_kernel(SimState S, int parity)
         }
     }
     __syncthreads();
-    if (t == 32 && S.totals_host) {   // this tile's largest world into the pinned mirror
+    if (t == 32 && S.totals_host && S.track_maxpop) {   // this tile's largest world into the pinned mirror
         int32_t mx = 0;
         for (int i = 0; i < 16; ++i) mx = max(mx, s_max[i]);
         __hip_atomic_store(S.totals_host + kTotMaxPop + b, (uint32_t)mx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);

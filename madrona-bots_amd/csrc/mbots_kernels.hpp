@@ -76,6 +76,8 @@ struct SimState {
     // overflow 128 slots), big_s: n > 128 (this step's sensor) -- each [2][W]
     // by step parity, with their counts in big_cnt[parity][2]
     uint32_t mixed;
+    uint32_t track_maxpop;          // K2 publishes each tile's largest world (kTotMaxPop; set by
+                                    // the first mbots_max_population)
     uint32_t list_par;              // the parity whose lists this launch reads (host-set)
     int32_t *big_k1, *big_s;
     uint32_t *big_cnt;

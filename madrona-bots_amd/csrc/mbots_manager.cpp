@@ -1607,7 +1607,11 @@ int mbots_max_population(mbots_handle *h, uint32_t *out)
         return MBOTS_OK;
     }
     HIP_TRY(hipSetDevice(h->device));
-    if (h->maxpop_stale) {   // (after a checkpoint load, until the next step's K2)
+    if (!h->S.track_maxpop) {   // the first call: K2 publishes the tile maxima from the next step on
+        h->S.track_maxpop = 1u;
+        h->maxpop_stale = true;
+    }
+    if (h->maxpop_stale) {   // (after a checkpoint load or before tracking, until the next step's K2)
         HIP_TRY(hipDeviceSynchronize());
         std::vector<int32_t> n(h->S.W);
         HIP_TRY(hipMemcpy(n.data(), h->S.n, n.size() * sizeof(int32_t), hipMemcpyDeviceToHost));
