@@ -60,14 +60,14 @@ extern "C" {
  * MBOTS_E_CAPACITY instead */
 #define MBOTS_FLAG_STRICT_CAPACITY  0x8u
 
-/* agent_capacity: 4..2048 slots per world (MBOTS_MAX_CAPACITY); the kernel
- * classes are 128 (default), 256, 512, 1024 and 2048 slots.  Up to 256 the
+/* agent_capacity: 4..4096 slots per world (MBOTS_MAX_CAPACITY); the kernel
+ * classes are 128 (default), 256, 512, 1024, 2048 and 4096 slots.  Up to 256 the
  * sensor's per-pixel depth key carries the object order (64 + slot for
  * agents) in the low 9 bits of a 32-bit word; the larger classes keep the same
  * quantised depth and the order in a 64-bit key, so a world renders the same
  * bytes in every class.  The K1 finder mode (<= 2048 worlds) is a <= 256-slot
  * mode. */
-#define MBOTS_MAX_CAPACITY          2048u
+#define MBOTS_MAX_CAPACITY          4096u
 
 /* execution modes (madrona::ExecMode; the reference's callers pick CPU when
  * no GPU is present, learn/env.py:12-15) */

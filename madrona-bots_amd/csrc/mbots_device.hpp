@@ -30,7 +30,7 @@ constexpr int kChunkW = 16;
 constexpr int kMaxPkg = 5;
 constexpr int kNumPkg = kNumChunks * kMaxPkg;   // 240 food packages per world
 constexpr int kFoodCap = 30;                  // totalAllowedFood
-constexpr int kMaxCap = 2048;                 // slot capacity bound (kernel classes 128 / 256 / ... / 2048)
+constexpr int kMaxCap = 4096;                 // slot capacity bound (kernel classes 128 / 256 / ... / 4096)
 constexpr float kLx = 128.0f;                 // 8 chunks * 16 cells * cellDim 1
 constexpr float kLy = 96.0f;
 // Quat::angleAxis(+-0.1, z) = (cos .05, 0, 0, +-sin .05), correctly rounded.

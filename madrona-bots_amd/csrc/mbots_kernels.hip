@@ -207,8 +207,9 @@ __device__ void world_step(SimState &S, const ObsTable &cur, WorldLDS<kCap> &L, 
 #define MB_K1_WPB 8   // 4: K1 +2.5 %, and +7 % step at 4096 worlds; 16: +30 % K1
 #endif
 constexpr int kK1Worlds = MB_K1_WPB;          // worlds (waves) per K1 block
-// per capacity class: the 512 / 1024 / 2048-slot images (17 / 34 / 66 KB of
-// LDS a world) take 4 / 2 / 1 worlds a block, two blocks per CU
+// per capacity class: the 512 / 1024 / 2048 / 4096-slot images (17 / 34 / 66 /
+// 131 KB of LDS a world) take 4 / 2 / 1 / 1 worlds a block (the 4096 image is the
+// largest the CU's 160 KB hold)
 template <int kCap>
 constexpr int k1_worlds() { return kCap <= 256 ? kK1Worlds : kCap == 512 ? 4 : kCap == 1024 ? 2 : 1; }
 template <int kCap>
@@ -1699,7 +1700,7 @@ constexpr int kSensorWorlds = MB_SENSOR_WPB;   // worlds (waves) per sensor bloc
 #define MB_SENSOR_SPLIT_WAVES MB_SENSOR_WPB   // waves per block of the split sensor
 #endif
 // the launch bounds' minimum waves per SIMD: 8 (<= 64 VGPRs) for the 128-slot
-// class, 4 for the 256-slot one, 2 for the 512 / 1024 classes, 1 for 2048 (LDS-bound there)
+// class, 4 for the 256-slot one, 2 for the 512 / 1024 classes, 1 for 2048 / 4096 (LDS-bound there)
 __host__ __device__ constexpr int sensor_min_waves(int cap) { return cap <= 128 ? 8 : cap <= 256 ? 4 : cap <= 1024 ? 2 : 1; }
 // kDepth: fix_depth_alias (a depth byte per pixel besides the semantic one).
 // kSplit: kSplit waves share one world, each taking every kSplit-th key chunk
@@ -2768,7 +2769,8 @@ hipError_t launch_world_step(const SimState &S, const ObsTable &cur, int parity,
             if (S.cap <= 256) list(world_step_list_kernel<256>, k1_worlds<256>());
             else if (S.cap <= 512) list(world_step_list_kernel<512>, k1_worlds<512>());
             else if (S.cap <= 1024) list(world_step_list_kernel<1024>, k1_worlds<1024>());
-            else list(world_step_list_kernel<2048>, k1_worlds<2048>());
+            else if (S.cap <= 2048) list(world_step_list_kernel<2048>, k1_worlds<2048>());
+            else list(world_step_list_kernel<4096>, k1_worlds<4096>());
         }
     } else if (S.cap <= 256)
         S.k1_finder ? go(world_step_kernel<256, true>, kK1Worlds) : go(world_step_kernel<256, false>, kK1Worlds);
@@ -2776,8 +2778,10 @@ hipError_t launch_world_step(const SimState &S, const ObsTable &cur, int parity,
         go(world_step_kernel<512, false>, k1_worlds<512>());
     else if (S.cap <= 1024)
         go(world_step_kernel<1024, false>, k1_worlds<1024>());
-    else
+    else if (S.cap <= 2048)
         go(world_step_kernel<2048, false>, k1_worlds<2048>());
+    else
+        go(world_step_kernel<4096, false>, k1_worlds<4096>());
     return hipGetLastError();
 }
 hipError_t launch_scan(const SimState &S, int parity, hipStream_t st, hipEvent_t done, bool plain_events)
@@ -2896,8 +2900,9 @@ static void launch_sensor_cap(const SimState &S, const ObsTable &nxt, hipStream_
 {
     const bool fixd = (S.flags & kFlagFixDepth) != 0;
     if constexpr (kCap > 256) {
-        // the large classes (11 / 21 / 38 KB of LDS a world at 512 / 1024 /
-        // 2048 slots): one wave per world, 2 / 1 / 1 worlds a block, no split
+        // the large classes (11 / 21 / 38 / 71 KB of LDS a world at 512 / 1024 /
+        // 2048 / 4096 slots): one wave per world, 2 / 1 / 1 / 1 worlds a block,
+        // no split
         constexpr int kWv = kCap > 512 ? 1 : 2;
         const dim3 grid((S.W + kWv - 1) / kWv), blk(64 * kWv);
         if (fixd) MB_LAUNCH_EV((sensor_kernel<true, 1, kCap, kWv>), grid, blk, st, done, plain_events, S, nxt);
@@ -2937,14 +2942,16 @@ hipError_t launch_sensor(const SimState &S, const ObsTable &nxt, hipStream_t st,
         if (S.cap <= 256) launch_sensor_list<256>(S, nxt, st, done, plain_events);
         else if (S.cap <= 512) launch_sensor_list<512>(S, nxt, st, done, plain_events);
         else if (S.cap <= 1024) launch_sensor_list<1024>(S, nxt, st, done, plain_events);
-        else launch_sensor_list<2048>(S, nxt, st, done, plain_events);
+        else if (S.cap <= 2048) launch_sensor_list<2048>(S, nxt, st, done, plain_events);
+        else launch_sensor_list<4096>(S, nxt, st, done, plain_events);
         return hipGetLastError();
     }
     if (S.cap <= 128) launch_sensor_cap<128>(S, nxt, st, done, plain_events);
     else if (S.cap <= 256) launch_sensor_cap<256>(S, nxt, st, done, plain_events);
     else if (S.cap <= 512) launch_sensor_cap<512>(S, nxt, st, done, plain_events);
     else if (S.cap <= 1024) launch_sensor_cap<1024>(S, nxt, st, done, plain_events);
-    else launch_sensor_cap<2048>(S, nxt, st, done, plain_events);
+    else if (S.cap <= 2048) launch_sensor_cap<2048>(S, nxt, st, done, plain_events);
+    else launch_sensor_cap<4096>(S, nxt, st, done, plain_events);
     return hipGetLastError();
 }
 hipError_t launch_shift(const SimState &S, const ObsTable &t, int mode, hipStream_t st)

@@ -116,8 +116,8 @@ def _check(rc):
 
 
 _W_CAPACITY, _E_CAPACITY = 1, -5   # include/mbots.h MBOTS_W_CAPACITY / MBOTS_E_CAPACITY
-MAX_CAPACITY = 2048                # MBOTS_MAX_CAPACITY
-CAPACITY_CLASSES = (128, 256, 512, 1024, 2048)   # the kernels' slot classes
+MAX_CAPACITY = 4096                # MBOTS_MAX_CAPACITY
+CAPACITY_CLASSES = (128, 256, 512, 1024, 2048, 4096)   # the kernels' slot classes
 
 
 def _capacity_class(need):
@@ -386,7 +386,7 @@ class SimManager:
     SURVEY B.1), shard_ghost (also step world world_offset + num_worlds, never
     exported, so a shard's faithful B.3 rewards equal one device's; its agents
     act on the write_synthetic_actions stream), strict_capacity (a world that
-    reaches agent_capacity -- at most MAX_CAPACITY = 2048 slots -- and drops a
+    reaches agent_capacity -- at most MAX_CAPACITY = 4096 slots -- and drops a
     birth or respawn makes step() raise CapacityError instead of warning with
     CapacityWarning: the reference has no cap).
 

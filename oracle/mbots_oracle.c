@@ -794,12 +794,14 @@ static orc_hit resolve(orc_hit h, int k, float ox, float oy, float hx, float hy)
     return out;
 }
 
-static void world_phase_d(orc_sim *s, uint32_t wi)
+/* the sensor of agents [lo, hi) of world wi: each agent writes only its own
+ * rows and finder, so agent ranges of one world run in parallel */
+static void world_phase_d_range(orc_sim *s, uint32_t wi, int32_t lo, int32_t hi)
 {
     orc_world *w = &s->w[wi];
     orc_cols *nc = &s->cur[s->tb ^ 1];
     orc_hit hits[ORC_SENSOR + 1];
-    for (int32_t i = 0; i < w->n; ++i) {
+    for (int32_t i = lo; i < hi; ++i) {
         orc_agent *a = &w->ag[i];
         float hx, hy;
         heading(a->rw, a->rz, &hx, &hy);
@@ -836,6 +838,40 @@ static void world_phase_d(orc_sim *s, uint32_t wi)
     }
 }
 
+/* the sensor over every world's agents, split evenly by agent count (a few
+ * worlds of thousands of agents still use every thread) */
+typedef struct { orc_sim *s; uint64_t lo, hi; } sensor_job_t;
+static void *sensor_job_run(void *p)
+{
+    sensor_job_t *j = (sensor_job_t *)p;
+    uint64_t g = 0;
+    for (uint32_t wi = 0; wi < j->s->cfg.num_worlds && g < j->hi; ++wi) {
+        uint64_t n = (uint64_t)j->s->w[wi].n, a = j->lo > g ? j->lo - g : 0, b = j->hi - g < n ? j->hi - g : n;
+        if (a < b) world_phase_d_range(j->s, wi, (int32_t)a, (int32_t)b);
+        g += n;
+    }
+    return NULL;
+}
+static void sensor_all(orc_sim *s)
+{
+    uint64_t G = 0;
+    for (uint32_t wi = 0; wi < s->cfg.num_worlds; ++wi) G += (uint64_t)s->w[wi].n;
+    uint32_t T = s->cfg.num_threads ? s->cfg.num_threads : 1;
+    if (T > 256) T = 256;
+    if ((uint64_t)T > G) T = G ? (uint32_t)G : 1;
+    pthread_t th[256];
+    sensor_job_t jobs[256];
+    for (uint32_t t = 0; t < T; ++t) {
+        jobs[t].s = s;
+        jobs[t].lo = G * t / T;
+        jobs[t].hi = G * (t + 1) / T;
+        if (T > 1) pthread_create(&th[t], NULL, sensor_job_run, &jobs[t]);
+    }
+    if (T <= 1) sensor_job_run(&jobs[0]);
+    else
+        for (uint32_t t = 0; t < T; ++t) pthread_join(th[t], NULL);
+}
+
 /* ------------------------------------------------------------------------ */
 /* Public API                                                                */
 /* ------------------------------------------------------------------------ */
@@ -843,7 +879,7 @@ static void finish_step(orc_sim *s)
 {
     compute_rows(s);
     for_worlds(s, world_phase_c);
-    for_worlds(s, world_phase_d);
+    sensor_all(s);
     s->tb ^= 1;
 }
 

@@ -140,10 +140,10 @@ class OracleSim:
         if not self._h:
             raise MemoryError("orc_create failed")
 
-    def __del__(self):
+    def __del__(self, _lib=lib):   # (bound now: module globals are gone at interpreter exit)
         h = getattr(self, "_h", None)
         if h:
-            lib().orc_destroy(h)
+            _lib().orc_destroy(h)
             self._h = None
 
     def step(self):

@@ -18,7 +18,7 @@ ap.add_argument("--warmup", type=int, default=200)
 ap.add_argument("--stream-priority", type=int, default=None,
                 help="run on a new torch stream of this priority (lower = higher priority)")
 ap.add_argument("--no-kernel-timing", action="store_true")
-ap.add_argument("--capacity", default="128", help='agent_capacity (kernel class 128 / 256 / 512 / 1024, or "auto")')
+ap.add_argument("--capacity", default="128", help='agent_capacity (kernel class 128 / 256 / 512 / 1024 / 2048 / 4096, or "auto")')
 a = ap.parse_args()
 if a.stream_priority is not None:
     torch.cuda.set_stream(torch.cuda.Stream(priority=a.stream_priority))

@@ -160,7 +160,7 @@ def test_breed_heavy_to_capacity_256():
     W = 16
     mgr = _mgr(W, agent_capacity=256)
     orc = pyoracle.OracleSim(W, 69, 32, cap=256, num_threads=4)
-    with pytest.warns(mb.CapacityWarning, match="at most 2048"):
+    with pytest.warns(mb.CapacityWarning, match=f"at most {mb.MAX_CAPACITY}"):
         _breed_steps(mgr, orc, 40)
     assert mgr.overflow() == orc.overflow() > 0
 

@@ -450,16 +450,17 @@ def _breed_heavy(n, step):
 
 
 @pytest.mark.parametrize("cap,W,steps", [(256, 48, 45), (128, 48, 45), (512, 16, 70), (1024, 8, 110),
-                                         (2048, 4, 190)])
+                                         (2048, 4, 190),
+                                         pytest.param(4096, 2, 255, marks=pytest.mark.timeout(600))])
 def test_capacity_classes_breed_heavy(cap, W, steps):
     """Worlds filling each kernel capacity class under a breed-heavy stream --
     128 and 256 slots (two / four 64-slot groups in K1 and the sensor), 512,
-    1024 and 2048 (4 / 2 / 1 worlds per K1 block, one wave per world in the
-    sensor, 64-bit depth keys): every column and the dropped-birth count equal
-    the oracle's after every step."""
+    1024, 2048 and 4096 (4 / 2 / 1 / 1 worlds per K1 block, one wave per world
+    in the sensor, 64-bit depth keys): every column and the dropped-birth count
+    equal the oracle's after every step."""
     import madrona_bots as mb
     mgr = mb.SimManager(0, W, 69, 32, agent_capacity=cap)
-    orc = pyoracle.OracleSim(W, 69, 32, cap=cap, num_threads=8)
+    orc = pyoracle.OracleSim(W, 69, 32, cap=cap, num_threads=16)
     peak = 0
     for t in range(steps):
         n = mgr.num_agents()
@@ -559,7 +560,8 @@ def test_checkpoint_across_capacities_gpu():
         mb.SimManager(0, 4100, 69, 32, agent_capacity=32).load_checkpoint(blob.tobytes())
 
 
-@pytest.mark.parametrize("cap,W,steps", [(512, 4100, 24), (256, 16400, 16), (1024, 3000, 20), (2048, 2100, 16)])
+@pytest.mark.parametrize("cap,W,steps", [(512, 4100, 24), (256, 16400, 16), (1024, 3000, 20), (2048, 2100, 16),
+                                         (4096, 2100, 16)])
 def test_mixed_classes_equal_single_class(cap, W, steps, monkeypatch):
     """Mixed capacity classes (the 128-slot K1 and sensor for every world that
     fits them, the class kernels for the worlds K2 lists) against the same
