@@ -453,9 +453,14 @@ class SimManager:
         if need <= self.agent_capacity:
             return
         blob = self.save_checkpoint()
-        old = self._hd
-        self._open(_capacity_class(need))
-        _check(_lib.mbots_load_checkpoint(self._h, ctypes.c_void_p(blob.ctypes.data), blob.size))
+        old = (self._hd, self._h, self.agent_capacity, self._cap_rows, self._views)
+        self._open(_capacity_class(need))   # (raises with the manager unchanged)
+        try:
+            _check(_lib.mbots_load_checkpoint(self._h, ctypes.c_void_p(blob.ctypes.data), blob.size))
+        except BaseException:
+            # keep running in the old class rather than on a fresh world
+            self._hd, self._h, self.agent_capacity, self._cap_rows, self._views = old
+            raise
         if self._ktiming:
             self.enable_kernel_timing(True)
         del old                      # (freed now unless a view still holds it)

@@ -199,6 +199,28 @@ def test_auto_capacity_grows_without_drops():
     assert mgr.overflow() == orc.overflow() == 0
 
 
+def test_auto_capacity_failed_growth_keeps_the_run(monkeypatch):
+    """A growth whose checkpoint load fails raises and leaves the manager in
+    its old class with its state (not a fresh world); the run then carries on,
+    grows once loads work again and stays equal to the oracle."""
+    import madrona_bots as mb
+    W = 8
+    mgr = _mgr(W, agent_capacity="auto")
+    orc = pyoracle.OracleSim(W, 69, 32, cap=1024, num_threads=4)
+    real = mb._lib.mbots_load_checkpoint
+    monkeypatch.setattr(mb._lib, "mbots_load_checkpoint", lambda *a: -1)
+    t = 0
+    with pytest.raises(RuntimeError):
+        while t < 80:
+            _breed_steps(mgr, orc, 1, t0=t)
+            t += 1
+    assert mgr.agent_capacity == 128 and mgr.num_agents() == orc.num_agents()
+    monkeypatch.setattr(mb._lib, "mbots_load_checkpoint", real)
+    _breed_steps(mgr, orc, 20, t0=t)
+    assert mgr.agent_capacity > 128
+    assert mgr.overflow() == orc.overflow() == 0
+
+
 def test_auto_capacity_old_views_keep_their_storage():
     _old_views_keep_storage("cpu")
 
