@@ -427,10 +427,11 @@ void Sim::export_world(uint32_t w, const Table &cur, Table &nxt, bool init)
 
 // the Sensor graph (sim.cpp:1183-1188; build spec DESIGN.md 3.6): every
 // (agent, object, ray) through the exact predicates -- K3b
-void Sim::sensor_world(uint32_t w, Table &nxt)
+void Sim::sensor_world(uint32_t w, Table &nxt, int lo, int hi)
 {
     const size_t base = (size_t)w * cap_;
     const int n = n_[w];
+    if (hi < 0) hi = n;
     const bool fixd = (cfg_.flags & MBOTS_FLAG_FIX_DEPTH_ALIAS) != 0;
     // live food in (chunk, package) order: position and rotation
     float2 fp[kNumPkg], fr[kNumPkg];
@@ -453,7 +454,7 @@ void Sim::sensor_world(uint32_t w, Table &nxt)
     for (int k = 0; k < kSensor; ++k) np[k] = near_pt(ray_u(k));
     np[kSensor] = finder_np();
     for (int i = 0; i < n; ++i) heading(rw_[base + i], rz_[base + i], hd[i].x, hd[i].y);
-    for (int i = 0; i < n; ++i) {
+    for (int i = lo; i < hi; ++i) {
         const float ax = x_[base + i], ay = y_[base + i];
         const float2 h = hd[i];
         // 64-bit keys in every capacity class (mbots_ray.hpp Key<>: the same
@@ -525,11 +526,42 @@ void Sim::step()
     Table &nxt = T_[tb_ ^ 1];
     for_worlds([&](uint32_t w) { world_step(w, cur); });
     scan();
-    for_worlds([&](uint32_t w) {
-        export_world(w, cur, nxt, false);
-        sensor_world(w, nxt);
-    });
+    if (W_ >= 2 * threads_) {
+        for_worlds([&](uint32_t w) {
+            export_world(w, cur, nxt, false);
+            sensor_world(w, nxt);
+        });
+    } else {   // few (large) worlds: the sensor split by agents over the threads
+        for_worlds([&](uint32_t w) { export_world(w, cur, nxt, false); });
+        sensor_by_agents(nxt);
+    }
     tb_ ^= 1;
+}
+
+// the sensor over every world's agents, split evenly by agent count: each
+// agent writes only its own rows and finder slot
+void Sim::sensor_by_agents(Table &nxt)
+{
+    uint64_t G = 0;
+    for (uint32_t w = 0; w < W_; ++w) G += (uint64_t)n_[w];
+    const unsigned T = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(threads_, G));
+    auto run = [&](uint64_t lo, uint64_t hi) {
+        uint64_t g = 0;
+        for (uint32_t w = 0; w < W_ && g < hi; ++w) {
+            const uint64_t n = (uint64_t)n_[w];
+            const uint64_t a = lo > g ? lo - g : 0, b = std::min(hi - g, n);
+            if (a < b) sensor_world(w, nxt, (int)a, (int)b);
+            g += n;
+        }
+    };
+    if (T == 1) {
+        run(0, G);
+        return;
+    }
+    std::vector<std::thread> th;
+    th.reserve(T);
+    for (unsigned t = 0; t < T; ++t) th.emplace_back(run, G * t / T, G * (t + 1) / T);
+    for (auto &t : th) t.join();
 }
 
 // shiftObservationsSystem + shiftHiddenState (sim.cpp:1002-1048)

@@ -67,7 +67,9 @@ private:
     void world_step(uint32_t w, const Table &cur);
     void scan();
     void export_world(uint32_t w, const Table &cur, Table &nxt, bool init);
-    void sensor_world(uint32_t w, Table &nxt);
+    // agents [lo, hi) of world w (hi < 0: all of them)
+    void sensor_world(uint32_t w, Table &nxt, int lo = 0, int hi = -1);
+    void sensor_by_agents(Table &nxt);
 
     mbots_config cfg_;
     uint32_t W_, Wx_, cap_, A_;   // simulated / exported worlds (W_ = Wx_ + the shard ghost)

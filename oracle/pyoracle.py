@@ -136,14 +136,15 @@ class OracleSim:
         self.cap = int(cap)
         cfg = _Cfg(num_worlds, world_offset, rand_seed, init_num_agents_per_world, cap,
                    1 if reward_fixed else 0, num_threads)
+        self._destroy = lib().orc_destroy
         self._h = lib().orc_create(ctypes.byref(cfg))
         if not self._h:
             raise MemoryError("orc_create failed")
 
-    def __del__(self, _lib=lib):   # (bound now: module globals are gone at interpreter exit)
+    def __del__(self):
         h = getattr(self, "_h", None)
         if h:
-            _lib().orc_destroy(h)
+            self._destroy(h)   # (held by the object: module globals are gone at interpreter exit)
             self._h = None
 
     def step(self):
