@@ -199,8 +199,8 @@ __device__ __forceinline__ void init_slot(WorldLDS<kCap> &L, int s, float x, flo
 // ---------------------------------------------------------------------------
 template <int kCap>
 struct FinderScratch;
-template <int kCap, bool kFinder>
-__device__ void world_step(SimState &S, const ObsTable &cur, WorldLDS<kCap> &L, FinderScratch<kCap> &F,
+template <int kCap, bool kFinder, bool kSkipBig = false>
+__device__ bool world_step(SimState &S, const ObsTable &cur, WorldLDS<kCap> &L, FinderScratch<kCap> &F,
                            uint32_t w, uint32_t lane);
 
 #ifndef MB_K1_WPB
@@ -235,8 +235,7 @@ __attribute__((amdgpu_num_sgpr(80))) void world_step_kernel(
     const uint32_t w = uniform(blockIdx.x * kW1 + wv);
     // (mixed classes: a world whose step could outgrow the small class is the
     // class kernel's, world_step_list_kernel)
-    const bool run = w < S.W && !(kSkipBig && k1_needs_class(uniform(S.n[w]), S.A));
-    if (run) world_step<kCap, kFinder>(S, cur, lds[wv], fsc[kFinder ? wv : 0], w, lane);
+    const bool run = w < S.W && world_step<kCap, kFinder, kSkipBig>(S, cur, lds[wv], fsc[kFinder ? wv : 0], w, lane);
     // counter-major tile buckets: [counter][tile][bucket] (K2 reads one
     // counter's buckets as contiguous 16-B words)
     const size_t nent = (size_t)S.ntiles * kTileBuckets;
@@ -506,14 +505,17 @@ __device__ void world_finders(const SimState &S, WorldLDS<kCap> &L, FinderScratc
     wave_sync();
 }
 
-template <int kCap, bool kFinder>
-__device__ void world_step(SimState &S, const ObsTable &cur, WorldLDS<kCap> &L, FinderScratch<kCap> &F,
+// returns false, having done nothing, for a world kSkipBig leaves to the
+// class kernel
+template <int kCap, bool kFinder, bool kSkipBig>
+__device__ bool world_step(SimState &S, const ObsTable &cur, WorldLDS<kCap> &L, FinderScratch<kCap> &F,
                            uint32_t w, uint32_t lane)
 {
     constexpr int kG = kCap / 64;   // 64-slot groups
     const uint32_t cap = S.cap;
     const size_t base = (size_t)w * cap;
     const int n0 = uniform(S.n[w]);
+    if (kSkipBig && k1_needs_class(n0, S.A)) return false;
 
     // ---- stage the world in LDS; slot `lane`'s action row is fetched now and
     // consumed after addFood (its latency hides behind that serial phase) ----
@@ -878,6 +880,7 @@ __device__ void world_step(SimState &S, const ObsTable &cur, WorldLDS<kCap> &L, 
             if (w < S.Wx) atomicAdd(&S.totals[kTotOverflow], ovf);
         }
     }
+    return true;
 }
 
 // ---------------------------------------------------------------------------
