@@ -2747,6 +2747,14 @@ hipError_t launch_tile_sum(const SimState &S, int parity, hipStream_t st)
     hipLaunchKernelGGL(tile_sum_kernel, dim3(S.ntiles), dim3(1024), 0, st, S, parity);
     return hipGetLastError();
 }
+// the class kernels' fixed grids (mixed classes): blocks looping over the
+// listed worlds -- a dispatch of them costs its empty blocks every step
+#ifndef MB_K1_LIST_BLOCKS
+#define MB_K1_LIST_BLOCKS 1024
+#endif
+#ifndef MB_SENSOR_LIST_BLOCKS
+#define MB_SENSOR_LIST_BLOCKS 2048
+#endif
 hipError_t launch_world_step(const SimState &S, const ObsTable &cur, int parity, hipStream_t st, hipEvent_t done)
 {
     auto go = [&](auto kern, int wpb) {
@@ -2765,7 +2773,8 @@ hipError_t launch_world_step(const SimState &S, const ObsTable &cur, int parity,
             hipLaunchKernelGGL((world_step_kernel<128, false, true>), dim3((S.W + kK1Worlds - 1) / kK1Worlds),
                                dim3(64 * kK1Worlds), 0, st, S, cur, parity);
             auto list = [&](auto kern, int wpb) {
-                const dim3 grid(std::max(1u, std::min((S.W + wpb - 1) / wpb, 1024u))), blk(64 * wpb);
+                const dim3 grid(std::max(1u, std::min((S.W + wpb - 1) / wpb, (unsigned)MB_K1_LIST_BLOCKS))),
+                    blk(64 * wpb);
                 if (!done) hipLaunchKernelGGL(kern, grid, blk, 0, st, S, cur, parity);
                 else hipExtLaunchKernelGGL(kern, grid, blk, 0u, st, nullptr, done, 0u, S, cur, parity);
             };
@@ -2931,7 +2940,7 @@ template <int kCap>
 static void launch_sensor_list(const SimState &S, const ObsTable &nxt, hipStream_t st, hipEvent_t done,
                                bool plain_events)
 {
-    const dim3 grid(std::max(1u, std::min(S.W, 2048u))), blk(64);
+    const dim3 grid(std::max(1u, std::min(S.W, (unsigned)MB_SENSOR_LIST_BLOCKS))), blk(64);
     if (S.flags & kFlagFixDepth)
         MB_LAUNCH_EV((sensor_kernel<true, 1, kCap, 1, true>), grid, blk, st, done, plain_events, S, nxt);
     else
